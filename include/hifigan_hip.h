@@ -1,0 +1,129 @@
+/*
+ * hifigan_hip.h — C ABI of libhifigan_hip.so, the MI355X (gfx950) HiFi-GAN
+ * Generator inference path.
+ *
+ * The reference has no FFI layer: its boundary is the PyTorch module
+ * HiFiGANGenerator (models/hifigan.py:134-283).  Each entry point below
+ * replaces one piece of that module's interface:
+ *
+ *   hfg_create          ← HiFiGANGenerator.__init__        models/hifigan.py:149-222
+ *                         (hyper-parameters only; no weights are created)
+ *   hfg_set_weight      ← load_state_dict of one key       (keys: SURVEY.md §8(b))
+ *                         incl. weight_g / weight_v from
+ *                         apply_weight_norm                models/hifigan.py:274-283
+ *   hfg_commit_weights  ← remove_weight_norm / fold        models/hifigan.py:263-272
+ *   hfg_forward[_ws]    ← HiFiGANGenerator.forward         models/hifigan.py:224-261
+ *   hfg_out_len         ← output-length contract           models/hifigan.py:195-203
+ *                         ((L-1)u - 2((k-u)//2) + k per stage)
+ *
+ * Conventions
+ *   - Every int-returning call returns 0 on success or a negative errno-style
+ *     code (HFG_E*), and sets a thread-local message read by hfg_last_error().
+ *     Nothing throws across the ABI.
+ *   - Tensors are fp32, contiguous, row-major: mel [B][n_mels][T],
+ *     wav [B][1][L] with L = hfg_out_len(h, T).  Both live in device memory
+ *     owned by the caller.  The input is never modified.
+ *   - hfg_forward* is asynchronous on the caller's HIP stream (hipStream_t
+ *     passed as void*; NULL = default stream): no host synchronisation and no
+ *     allocation when weights are committed and the workspace is large enough,
+ *     so it may be captured into a hipGraph.
+ *   - One handle per device.  A handle is not thread-safe; hfg_forward with
+ *     the internal workspace must not run concurrently on two streams —
+ *     use hfg_forward_ws with a per-stream workspace for that.
+ */
+#ifndef HIFIGAN_HIP_H
+#define HIFIGAN_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define HFG_MAX_STAGES 8
+#define HFG_MAX_RES 8
+#define HFG_MAX_DIL 8
+
+#define HFG_OK 0
+#define HFG_EINVAL (-22)   /* bad argument / shape / unknown key          */
+#define HFG_ENOMEM (-12)   /* device allocation failed                    */
+#define HFG_ENODEV (-19)   /* no HIP device / bad device index            */
+#define HFG_EAGAIN (-11)   /* weights incomplete (a key was never set)    */
+#define HFG_EIO (-5)       /* HIP runtime error (launch, memcpy, ...)     */
+
+typedef struct hfg_handle hfg_handle;
+
+/* Hyper-parameters: models/hifigan.py:149-158 constructor arguments. */
+typedef struct hfg_config {
+    int32_t n_mels;                              /* 80                        */
+    int32_t n_up;                                /* len(upsample_rates)       */
+    int32_t up_rates[HFG_MAX_STAGES];            /* [8, 8, 2, 2]              */
+    int32_t up_kernels[HFG_MAX_STAGES];          /* [16, 16, 4, 4]            */
+    int32_t c0;                                  /* upsample_initial_channel  */
+    int32_t n_res;                               /* len(resblock_kernel_sizes) */
+    int32_t res_kernels[HFG_MAX_RES];            /* [3, 7, 11]                */
+    int32_t n_dil[HFG_MAX_RES];                  /* len(dilations[j])         */
+    int32_t dil[HFG_MAX_RES][HFG_MAX_DIL];       /* [[1,3,5],[1,3,5],[1,3,5]] */
+    int32_t dtype;                               /* 0 = fp32 (only value)     */
+} hfg_config;
+
+/* Library version string, e.g. "hifigan_hip 0.1.0 gfx950". */
+const char* hfg_version(void);
+
+/* Message of the last failing call on this thread ("" if none). */
+const char* hfg_last_error(void);
+
+/* Validate cfg, select `device` (hipSetDevice) and create a handle. */
+int hfg_create(const hfg_config* cfg, int device, hfg_handle** out);
+
+void hfg_destroy(hfg_handle* h);
+
+/* Number of parameter tensors (state_dict keys without weight norm). */
+int hfg_num_params(const hfg_handle* h);
+
+/* Load one state_dict tensor by its reference key, e.g.
+ * "mrfs.1.resblocks.2.convs1.0.weight".  `data` is fp32 contiguous, host
+ * memory (is_device = 0) or device memory (is_device = 1, copied D2H with
+ * a synchronous hipMemcpy).  Keys ending in weight_g / weight_v are folded
+ * as w = g * v / ||v|| (norm over all dims but 0) once both are present.
+ * Shapes are checked against the configuration. */
+int hfg_set_weight(hfg_handle* h, const char* name, const void* data,
+                   const int64_t* shape, int ndim, int is_device);
+
+/* Pack every layer into the kernels' fragment-ordered layout and upload it
+ * (synchronous).  Returns HFG_EAGAIN if a key was never set.  hfg_forward
+ * commits implicitly when weights changed since the last commit. */
+int hfg_commit_weights(hfg_handle* h);
+
+/* Output length for T mel frames (T * prod(up_rates) for exact configs). */
+int64_t hfg_out_len(const hfg_handle* h, int64_t T);
+
+/* Bytes of device workspace hfg_forward_ws needs for a [B, n_mels, T] input. */
+size_t hfg_workspace_bytes(const hfg_handle* h, int64_t B, int64_t T);
+
+/* Grow the internal workspace to fit [B, n_mels, T] (synchronous alloc). */
+int hfg_reserve(hfg_handle* h, int64_t B, int64_t T);
+
+/* wav[B][1][out_len] = Generator(mel[B][n_mels][T]); internal workspace. */
+int hfg_forward(hfg_handle* h, const float* mel, int64_t B, int64_t T,
+                float* wav, int64_t out_len, void* stream);
+
+/* Same with a caller-provided device workspace of >= hfg_workspace_bytes. */
+int hfg_forward_ws(hfg_handle* h, const float* mel, int64_t B, int64_t T,
+                   float* wav, int64_t out_len, void* workspace,
+                   size_t workspace_bytes, void* stream);
+
+/* Per-launch profiling with HIP events recorded on the launch stream.
+ * While enabled, every kernel launch of hfg_forward* is bracketed by an
+ * event pair.  hfg_profile_summary synchronises on the recorded events and
+ * writes a JSON object {kernel_label: {"launches", "ms", "flop", "bytes"}}
+ * (algorithmic FLOP and bytes) into buf. */
+int hfg_set_profiling(hfg_handle* h, int enable);
+int hfg_profile_reset(hfg_handle* h);
+int hfg_profile_summary(hfg_handle* h, char* buf, size_t buflen);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* HIFIGAN_HIP_H */

@@ -1,0 +1,31 @@
+/*
+ * hifigan_hip_inspect.h — host-only inspection entry points of
+ * libhifigan_hip.so, used by the CPU test-suite to check weight packing
+ * without a GPU.  Not part of the reference-facing boundary
+ * (include/hifigan_hip.h); a handle created with device = -1 is host-only:
+ * it validates the configuration, accepts hfg_set_weight with host data and
+ * packs weights, but cannot run hfg_forward*.
+ */
+#ifndef HIFIGAN_HIP_INSPECT_H
+#define HIFIGAN_HIP_INSPECT_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "hifigan_hip.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Copy the packed image of one layer (module prefix, e.g. "ups.0") into out:
+ * w_len packed GEMM weights followed by b_len per-row biases.  info[8]
+ * receives {kind (0 conv, 1 ups, 2 post), M, KT, tile, m_tiles, n_chunks,
+ * w_len, b_len}.  With out == NULL only info is filled. */
+int hfg_debug_packed_layer(hfg_handle* h, const char* mod, float* out, size_t cap,
+                           int64_t* info);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* HIFIGAN_HIP_INSPECT_H */

@@ -1,0 +1,200 @@
+"""C ABI on the CPU container: the library loads, exports every symbol the
+headers declare, validates configurations, and packs weights into exactly the
+GEMM layout the kernels consume (checked by a numpy emulation of the kernels'
+implicit GEMM, incl. the polyphase ConvTranspose1d).  No compute call needs a
+GPU: handles are host-only (device = -1)."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from conftest import ROOT
+from oracle import config as C
+
+# kTiles of csrc/kernels.h: (WM, WN, WAVES_M, WAVES_N, CK)
+TILES = [(2, 2, 2, 2, 8), (2, 2, 1, 4, 8), (1, 4, 1, 4, 8)]
+
+
+def header_symbols():
+    syms = set()
+    for h in ("hifigan_hip.h", "hifigan_hip_inspect.h"):
+        src = open(os.path.join(ROOT, "include", h)).read()
+        src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+        syms |= set(re.findall(r"\b(hfg_[a-z_]+)\s*\(", src))
+    return syms
+
+
+def test_library_exports_every_header_symbol(pkg):
+    lib = pkg.load_library()
+    syms = header_symbols()
+    assert len(syms) == 16
+    for s in sorted(syms):
+        assert hasattr(lib, s), f"missing export {s}"
+    assert set(syms) == set(pkg._lib.SIGNATURES), "ctypes signatures out of sync with headers"
+    assert b"gfx950" in lib.hfg_version()
+
+
+def host_handle(pkg, cfg):
+    c = pkg.make_config(**{k: v for k, v in cfg.kwargs().items()})
+    return pkg.Handle(c, -1)
+
+
+def test_create_validates_config(pkg):
+    lib = pkg.load_library()
+    c = pkg.make_config(80, [8, 8, 2, 2], [16, 16, 4, 4], 512, [3, 7, 11], [[1, 3, 5]] * 3)
+    c.dtype = 1
+    h = ctypes.c_void_p()
+    assert lib.hfg_create(ctypes.byref(c), -1, ctypes.byref(h)) == -22
+    assert b"dtype" in lib.hfg_last_error()
+    c.dtype = 0
+    c.up_rates[0] = 0
+    assert lib.hfg_create(ctypes.byref(c), -1, ctypes.byref(h)) == -22
+    assert lib.hfg_create(None, -1, ctypes.byref(h)) == -22
+
+
+def test_out_len_and_workspace(pkg):
+    for cfg in (C.V1, C.V2STAR, C.NONEXACT):
+        h = host_handle(pkg, cfg)
+        for t in (1, 17, 256):
+            assert h.out_len(t) == C.out_len(cfg, t)
+        assert h.workspace_bytes(8, 1024) >= 4 * 4 * 8 * 128 * 65536 * (cfg is C.V1)
+    h = host_handle(pkg, C.V1)
+    assert h.workspace_bytes(8, 1024) == 4 * 4 * 8 * 128 * 65536
+    assert pkg.load_library().hfg_num_params(h.ptr) == 156
+
+
+def test_set_weight_errors_and_commit(pkg):
+    h = host_handle(pkg, C.V2STAR)
+    sd = C.make_state_dict(C.V2STAR, seed=3)
+    with pytest.raises(pkg.HfgError) as e:
+        h.set_weight("conv_pre.nope", torch.zeros(3))
+    assert e.value.code == -22
+    with pytest.raises(pkg.HfgError):
+        h.set_weight("conv_pre.weight", torch.zeros(128, 80, 5))  # wrong k
+    with pytest.raises(pkg.HfgError) as e:
+        h.commit()  # nothing set yet
+    assert e.value.code == -11
+    for k, v in sd.items():
+        h.set_weight(k, torch.from_numpy(v))
+    h.commit()
+    lib = pkg.load_library()
+    rc = lib.hfg_forward(h.ptr, None, 1, 4, None, 1024, None)
+    assert rc == -22  # host-only handle: no forward
+
+
+def unpack_gemm(info, packed, cin):
+    """Invert the fragment order of conv_kernels.hip → Wt[row][ci][j]."""
+    WM, WN, WAVES_M, WAVES_N, CK = TILES[info["tile"]]
+    MT = 32 * WM * WAVES_M
+    KK = CK // 2
+    KT = info["KT"]
+    shape = (info["m_tiles"], info["n_chunks"], KT, KK, WAVES_M, 64, WM)
+    p = packed.reshape(shape)
+    Wt = np.zeros((info["m_tiles"] * MT, info["n_chunks"] * CK, KT), np.float32)
+    lane = np.arange(64)
+    for mt in range(shape[0]):
+        for c in range(shape[1]):
+            for j in range(KT):
+                for kk in range(KK):
+                    for wv in range(WAVES_M):
+                        for wm in range(WM):
+                            rows = mt * MT + wv * 32 * WM + wm * 32 + (lane & 31)
+                            cis = c * CK + 2 * kk + (lane >> 5)
+                            Wt[rows, cis, j] = p[mt, c, j, kk, wv, :, wm]
+    return Wt[: info["M"], :cin, :]
+
+
+def emulate_conv(Wt, bias_rows, x, off, dil, N):
+    """out[m][n] = bias[m] + sum_{ci,j} Wt[m][ci][j] * x[ci][n + off + j*dil] (zero padded)."""
+    cin, L = x.shape
+    M, _, KT = Wt.shape
+    out = np.tile(bias_rows[:M, None].astype(np.float64), (1, N))
+    for j in range(KT):
+        idx = np.arange(N) + off + j * dil
+        ok = (idx >= 0) & (idx < L)
+        xs = np.zeros((cin, N))
+        xs[:, ok] = x[:, idx[ok]]
+        out += Wt[:, :, j].astype(np.float64) @ xs
+    return out
+
+
+@pytest.mark.parametrize("preset", ["v1", "v2star", "nonexact"])
+def test_packing_emulates_conv_and_polyphase_upsample(pkg, preset):
+    cfg = C.PRESETS[preset]
+    sd = C.make_state_dict(cfg, seed=21)
+    h = host_handle(pkg, cfg)
+    for k, v in sd.items():
+        h.set_weight(k, torch.from_numpy(v))
+    h.commit()
+    rng = np.random.default_rng(0)
+    c0 = cfg.upsample_initial_channel
+    # every upsample layer: polyphase GEMM + scatter == F.conv_transpose1d
+    for i, (u, k) in enumerate(zip(cfg.upsample_rates, cfg.upsample_kernel_sizes)):
+        cin, cout = c0 >> i, c0 >> (i + 1)
+        info, packed, bias = pkg_layer(h, f"ups.{i}")
+        assert info["kind"] == 1 and info["M"] == cout * u and info["KT"] == -(-k // u)
+        Wt = unpack_gemm(info, packed, cin)
+        Lin = 13
+        x = rng.standard_normal((cin, Lin)).astype(np.float32)
+        ref = F.conv_transpose1d(torch.from_numpy(x)[None], torch.from_numpy(sd[f"ups.{i}.weight"]),
+                                 torch.from_numpy(sd[f"ups.{i}.bias"]), u, (k - u) // 2)[0].numpy()
+        Lout = ref.shape[-1]
+        p = (k - u) // 2
+        N = (Lout - 1 + p) // u + 1
+        g = emulate_conv(Wt, bias, x, -(info["KT"] - 1), 1, N)
+        y = np.full((cout, Lout), np.nan)
+        for m in range(cout * u):
+            co, r = divmod(m, u)
+            t = np.arange(N) * u + r - p
+            ok = (t >= 0) & (t < Lout)
+            y[co, t[ok]] = g[m, ok]
+        assert not np.isnan(y).any()
+        assert np.abs(y - ref).max() < 1e-4
+    # one dilated ResBlock conv of each stage: GEMM == F.conv1d
+    for i in range(len(cfg.upsample_rates)):
+        ch = c0 >> (i + 1)
+        kr, d = cfg.resblock_kernel_sizes[-1], cfg.resblock_dilation_sizes[-1][-1]
+        mod = f"mrfs.{i}.resblocks.{len(cfg.resblock_kernel_sizes) - 1}.convs1.{len(cfg.resblock_dilation_sizes[-1]) - 1}"
+        info, packed, bias = pkg_layer(h, mod)
+        assert info["kind"] == 0 and info["M"] == ch and info["KT"] == kr
+        Wt = unpack_gemm(info, packed, ch)
+        x = rng.standard_normal((ch, 40)).astype(np.float32)
+        pad = C.get_padding(kr, d)
+        ref = F.conv1d(torch.from_numpy(x)[None], torch.from_numpy(sd[mod + ".weight"]),
+                       torch.from_numpy(sd[mod + ".bias"]), 1, pad, d)[0].numpy()
+        g = emulate_conv(Wt, bias, x, -pad, d, 40)
+        assert np.abs(g - ref).max() < 1e-4
+
+
+def pkg_layer(h, mod):
+    return h.packed_layer(mod)
+
+
+def test_weight_norm_fold(pkg):
+    cfg = C.V2STAR
+    wn = C.make_weight_norm_state_dict(cfg, seed=5)
+    plain = {}
+    for k, v in wn.items():
+        if k.endswith("weight_g"):
+            mod = k[:-9]
+            vv = wn[mod + ".weight_v"].astype(np.float64)
+            norm = np.sqrt((vv ** 2).reshape(vv.shape[0], -1).sum(1)).reshape(v.shape)
+            plain[mod + ".weight"] = (v * vv / norm).astype(np.float32)
+        elif not k.endswith("weight_v"):
+            plain[k] = v
+    h1, h2 = host_handle(pkg, cfg), host_handle(pkg, cfg)
+    for k, v in wn.items():
+        h1.set_weight(k, torch.from_numpy(v))
+    for k, v in plain.items():
+        h2.set_weight(k, torch.from_numpy(v))
+    h1.commit()
+    h2.commit()
+    for mod in ("ups.1", "mrfs.2.resblocks.1.convs2.0", "conv_pre", "conv_post"):
+        _, a, ab = h1.packed_layer(mod)
+        _, b, bb = h2.packed_layer(mod)
+        assert np.allclose(a, b, rtol=1e-6, atol=1e-7)
+        assert np.array_equal(ab, bb)

@@ -1,0 +1,199 @@
+"""ctypes binding of libhifigan_hip.so (C ABI: include/hifigan_hip.h).
+
+The library is the product path; there is no fallback.  Loading fails loudly
+when the .so is missing (build it with ``__graft_entry__.build()`` or
+``python tts-sambert_hifigan_amd/build.py``).
+
+``torch`` is imported before the library is opened so that the library's
+``libamdhip64.so.7`` dependency binds to the HIP runtime torch already loaded
+(same SONAME) — one HIP runtime per process, and torch's streams and device
+pointers are valid handles for the library.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import (POINTER, c_char_p, c_int, c_int32, c_int64, c_size_t, c_void_p,
+                    c_float)
+
+import torch  # noqa: F401  (see module docstring: bind torch's HIP runtime first)
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(PKG_DIR, "libhifigan_hip.so")
+
+HFG_MAX_STAGES = 8
+HFG_MAX_RES = 8
+HFG_MAX_DIL = 8
+
+ERRORS = {0: "OK", -22: "EINVAL", -12: "ENOMEM", -19: "ENODEV", -11: "EAGAIN", -5: "EIO"}
+
+
+class HipExtensionMissing(RuntimeError):
+    pass
+
+
+class HfgError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"hifigan_hip error {code} ({ERRORS.get(code, '?')}): {msg}")
+        self.code = code
+
+
+class HfgConfig(ctypes.Structure):
+    _fields_ = [
+        ("n_mels", c_int32),
+        ("n_up", c_int32),
+        ("up_rates", c_int32 * HFG_MAX_STAGES),
+        ("up_kernels", c_int32 * HFG_MAX_STAGES),
+        ("c0", c_int32),
+        ("n_res", c_int32),
+        ("res_kernels", c_int32 * HFG_MAX_RES),
+        ("n_dil", c_int32 * HFG_MAX_RES),
+        ("dil", (c_int32 * HFG_MAX_DIL) * HFG_MAX_RES),
+        ("dtype", c_int32),
+    ]
+
+
+def make_config(n_mels, upsample_rates, upsample_kernel_sizes, upsample_initial_channel,
+                resblock_kernel_sizes, resblock_dilation_sizes) -> HfgConfig:
+    if len(upsample_rates) != len(upsample_kernel_sizes):
+        raise ValueError("upsample_rates and upsample_kernel_sizes differ in length")
+    if len(resblock_kernel_sizes) != len(resblock_dilation_sizes):
+        # the reference zips them (models/hifigan.py:106); keep its truncation semantics
+        n = min(len(resblock_kernel_sizes), len(resblock_dilation_sizes))
+        resblock_kernel_sizes = list(resblock_kernel_sizes)[:n]
+        resblock_dilation_sizes = list(resblock_dilation_sizes)[:n]
+    if len(upsample_rates) > HFG_MAX_STAGES or len(resblock_kernel_sizes) > HFG_MAX_RES:
+        raise ValueError("configuration exceeds the ABI's stage / resblock limits")
+    c = HfgConfig()
+    c.n_mels = int(n_mels)
+    c.n_up = len(upsample_rates)
+    for i, (u, k) in enumerate(zip(upsample_rates, upsample_kernel_sizes)):
+        c.up_rates[i] = int(u)
+        c.up_kernels[i] = int(k)
+    c.c0 = int(upsample_initial_channel)
+    c.n_res = len(resblock_kernel_sizes)
+    for j, (k, dils) in enumerate(zip(resblock_kernel_sizes, resblock_dilation_sizes)):
+        if len(dils) > HFG_MAX_DIL:
+            raise ValueError("too many dilations in one ResBlock")
+        c.res_kernels[j] = int(k)
+        c.n_dil[j] = len(dils)
+        for m, d in enumerate(dils):
+            c.dil[j][m] = int(d)
+    c.dtype = 0
+    return c
+
+
+_lib = None
+
+# name -> (restype, argtypes); every symbol declared in include/hifigan_hip*.h
+SIGNATURES = {
+    "hfg_version": (c_char_p, []),
+    "hfg_last_error": (c_char_p, []),
+    "hfg_create": (c_int, [POINTER(HfgConfig), c_int, POINTER(c_void_p)]),
+    "hfg_destroy": (None, [c_void_p]),
+    "hfg_num_params": (c_int, [c_void_p]),
+    "hfg_set_weight": (c_int, [c_void_p, c_char_p, c_void_p, POINTER(c_int64), c_int, c_int]),
+    "hfg_commit_weights": (c_int, [c_void_p]),
+    "hfg_out_len": (c_int64, [c_void_p, c_int64]),
+    "hfg_workspace_bytes": (c_size_t, [c_void_p, c_int64, c_int64]),
+    "hfg_reserve": (c_int, [c_void_p, c_int64, c_int64]),
+    "hfg_forward": (c_int, [c_void_p, c_void_p, c_int64, c_int64, c_void_p, c_int64, c_void_p]),
+    "hfg_forward_ws": (c_int, [c_void_p, c_void_p, c_int64, c_int64, c_void_p, c_int64,
+                               c_void_p, c_size_t, c_void_p]),
+    "hfg_set_profiling": (c_int, [c_void_p, c_int]),
+    "hfg_profile_reset": (c_int, [c_void_p]),
+    "hfg_profile_summary": (c_int, [c_void_p, c_char_p, c_size_t]),
+    "hfg_debug_packed_layer": (c_int, [c_void_p, c_char_p, POINTER(c_float), c_size_t,
+                                       POINTER(c_int64)]),
+}
+
+
+def load_library(path: str = LIB_PATH):
+    """Open libhifigan_hip.so (cached).  Raises HipExtensionMissing if absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise HipExtensionMissing(
+            f"{path} is missing: the HIP extension must be built first "
+            "(python tts-sambert_hifigan_amd/build.py). There is no CPU fallback.")
+    lib = ctypes.CDLL(path)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def check(rc: int):
+    if rc != 0:
+        msg = load_library().hfg_last_error().decode(errors="replace")
+        raise HfgError(rc, msg)
+    return rc
+
+
+class Handle:
+    """Owning wrapper of an ``hfg_handle*`` (one per device)."""
+
+    def __init__(self, cfg: HfgConfig, device: int):
+        self.lib = load_library()
+        self.device = device
+        h = c_void_p()
+        check(self.lib.hfg_create(ctypes.byref(cfg), int(device), ctypes.byref(h)))
+        self.ptr = h
+
+    def __del__(self):
+        try:
+            if getattr(self, "ptr", None):
+                self.lib.hfg_destroy(self.ptr)
+                self.ptr = None
+        except Exception:
+            pass
+
+    def set_weight(self, name: str, t: "torch.Tensor"):
+        t = t.detach()
+        is_dev = 1 if t.is_cuda else 0
+        t = t.to(torch.float32).contiguous()
+        shape = (c_int64 * max(t.dim(), 1))(*t.shape)
+        check(self.lib.hfg_set_weight(self.ptr, name.encode(), c_void_p(t.data_ptr()), shape,
+                                      t.dim(), is_dev))
+
+    def commit(self):
+        check(self.lib.hfg_commit_weights(self.ptr))
+
+    def out_len(self, T: int) -> int:
+        return int(self.lib.hfg_out_len(self.ptr, int(T)))
+
+    def workspace_bytes(self, B: int, T: int) -> int:
+        return int(self.lib.hfg_workspace_bytes(self.ptr, int(B), int(T)))
+
+    def forward_ws(self, mel_ptr: int, B: int, T: int, wav_ptr: int, out_len: int, ws_ptr: int,
+                   ws_bytes: int, stream: int):
+        check(self.lib.hfg_forward_ws(self.ptr, c_void_p(mel_ptr), int(B), int(T),
+                                      c_void_p(wav_ptr), int(out_len), c_void_p(ws_ptr),
+                                      int(ws_bytes), c_void_p(stream)))
+
+    def set_profiling(self, on: bool):
+        check(self.lib.hfg_set_profiling(self.ptr, 1 if on else 0))
+
+    def profile_reset(self):
+        check(self.lib.hfg_profile_reset(self.ptr))
+
+    def profile_summary(self) -> dict:
+        import json
+        buf = ctypes.create_string_buffer(1 << 16)
+        check(self.lib.hfg_profile_summary(self.ptr, buf, len(buf)))
+        return json.loads(buf.value.decode())
+
+    def packed_layer(self, mod: str):
+        """(info dict, packed weights np.ndarray, per-row bias np.ndarray) of one layer."""
+        import numpy as np
+        info = (c_int64 * 8)()
+        check(self.lib.hfg_debug_packed_layer(self.ptr, mod.encode(), None, 0, info))
+        w_len, b_len = int(info[6]), int(info[7])
+        out = np.zeros(w_len + b_len, dtype=np.float32)
+        check(self.lib.hfg_debug_packed_layer(
+            self.ptr, mod.encode(), out.ctypes.data_as(POINTER(c_float)), out.size, info))
+        keys = ["kind", "M", "KT", "tile", "m_tiles", "n_chunks", "w_len", "b_len"]
+        return dict(zip(keys, [int(v) for v in info])), out[:w_len], out[w_len:]

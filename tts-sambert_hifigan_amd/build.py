@@ -1,0 +1,54 @@
+"""Build libhifigan_hip.so in-tree with hipcc for gfx950 (no torch, no JIT cache).
+
+    python tts-sambert_hifigan_amd/build.py          # or __graft_entry__.build()
+"""
+from __future__ import annotations
+
+import os
+import subprocess
+import sys
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(PKG_DIR, "csrc")
+LIB_NAME = "libhifigan_hip.so"
+LIB_PATH = os.path.join(PKG_DIR, LIB_NAME)
+SOURCES = ["conv_kernels.hip", "hifigan_capi.cpp"]
+HEADERS = ["kernels.h", os.path.join("..", "..", "include", "hifigan_hip.h"),
+           os.path.join("..", "..", "include", "hifigan_hip_inspect.h")]
+
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+FLAGS = [
+    "--offload-arch=gfx950",
+    # code object v5: loadable by both /opt/rocm (7.2) and torch's bundled HIP runtime
+    "-mcode-object-version=5",
+    "-O3", "-std=c++17", "-fPIC", "-shared",
+    "-Wall", "-Wno-unused-result",
+]
+
+
+def _stale() -> bool:
+    if not os.path.exists(LIB_PATH):
+        return True
+    t = os.path.getmtime(LIB_PATH)
+    deps = [os.path.join(CSRC, s) for s in SOURCES] + [os.path.join(CSRC, h) for h in HEADERS]
+    return any(os.path.exists(d) and os.path.getmtime(d) > t for d in deps)
+
+
+def build(force: bool = False, verbose: bool = True) -> str:
+    """Compile the HIP kernels + C ABI into ``libhifigan_hip.so`` next to this file."""
+    if not force and not _stale():
+        return LIB_PATH
+    tmp = LIB_PATH + ".tmp"
+    cmd = [HIPCC, *FLAGS, *[os.path.join(CSRC, s) for s in SOURCES], "-o", tmp]
+    if verbose:
+        print("[build]", " ".join(cmd), flush=True)
+    res = subprocess.run(cmd, capture_output=True, text=True)
+    if res.returncode != 0:
+        sys.stderr.write(res.stdout + res.stderr)
+        raise RuntimeError(f"hipcc failed with exit code {res.returncode}")
+    os.replace(tmp, LIB_PATH)
+    return LIB_PATH
+
+
+if __name__ == "__main__":
+    print(build(force="--force" in sys.argv))

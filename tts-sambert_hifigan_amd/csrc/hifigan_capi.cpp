@@ -1,0 +1,790 @@
+// hifigan_capi.cpp — C ABI (include/hifigan_hip.h) and host orchestration of the
+// MI355X HiFi-GAN Generator: parameter store keyed by the reference state_dict
+// names, weight-norm folding, packing into the MFMA fragment order, workspace
+// management and the 78-launch forward schedule of
+// HiFiGANGenerator.forward (models/hifigan.py:224-261).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "../../include/hifigan_hip.h"
+#include "../../include/hifigan_hip_inspect.h"
+#include "kernels.h"
+
+using hfg::ConvParams;
+using hfg::kTiles;
+using hfg::TileCfg;
+using hfg::TileId;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return code;
+}
+
+int hip_fail(hipError_t e, const char* what) {
+  return fail(HFG_EIO, "%s: %s", what, hipGetErrorString(e));
+}
+
+// models/hifigan.py:21-23
+int get_padding(int k, int d) { return (int)((k * d - d) / 2); }
+
+enum LayerKind { L_CONV, L_UPS, L_POST };
+
+struct Layer {
+  LayerKind kind;
+  std::string mod;   // state_dict module prefix
+  int C_in, C_out, k, dil, pad;
+  int s, p;          // ConvTranspose1d stride / padding
+  // GEMM view
+  int M, KT, tile, m_tiles, n_chunks;
+  size_t w_off, b_off;  // offsets (floats) into the packed device buffer
+  size_t w_len, b_len;
+};
+
+struct Param {
+  std::vector<int64_t> shape;
+  std::vector<float> data;
+  bool set = false;
+};
+
+struct ProfRec {
+  const char* label;
+  double flop, bytes;
+  hipEvent_t e0, e1;
+};
+
+struct Stage {
+  int conv_ups;               // index of the ups layer
+  std::vector<int> conv1;     // [j*n_dil + m]
+  std::vector<int> conv2;
+};
+
+}  // namespace
+
+struct hfg_handle {
+  hfg_config cfg;
+  int device;  // -1: host-only handle (validation / packing inspection)
+  std::vector<Layer> layers;
+  int conv_pre = -1, conv_post = -1;
+  std::vector<Stage> stages;
+  std::map<std::string, Param> params;       // "<mod>.weight" / "<mod>.bias"
+  std::map<std::string, Param> wn_parts;     // "<mod>.weight_g" / "<mod>.weight_v"
+  std::vector<std::string> param_order;
+  bool dirty = true;
+  std::vector<float> packed_host;
+  float* packed_dev = nullptr;
+  size_t packed_dev_len = 0;
+  void* ws = nullptr;
+  size_t ws_bytes = 0;
+  bool profiling = false;
+  std::vector<ProfRec> prof;
+  std::vector<hipEvent_t> event_pool;
+};
+
+namespace {
+
+struct DeviceGuard {
+  int prev = -1;
+  bool ok = true;
+  explicit DeviceGuard(int dev) {
+    if (dev < 0) return;
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    if (prev != dev) ok = hipSetDevice(dev) == hipSuccess;
+  }
+  ~DeviceGuard() {
+    int cur = -1;
+    if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+  }
+};
+
+int validate_config(const hfg_config* c) {
+  if (!c) return fail(HFG_EINVAL, "config is NULL");
+  if (c->n_mels <= 0) return fail(HFG_EINVAL, "n_mels must be > 0");
+  if (c->n_up <= 0 || c->n_up > HFG_MAX_STAGES) return fail(HFG_EINVAL, "n_up out of range");
+  if (c->n_res <= 0 || c->n_res > HFG_MAX_RES) return fail(HFG_EINVAL, "n_res out of range");
+  if (c->dtype != 0) return fail(HFG_EINVAL, "only dtype 0 (fp32) is supported");
+  if (c->c0 <= 0) return fail(HFG_EINVAL, "upsample_initial_channel must be > 0");
+  for (int i = 0; i < c->n_up; ++i) {
+    if (c->up_rates[i] <= 0 || c->up_kernels[i] <= 0)
+      return fail(HFG_EINVAL, "upsample rate/kernel %d must be > 0", i);
+    if ((c->c0 >> (i + 1)) <= 0) return fail(HFG_EINVAL, "channels vanish at stage %d", i);
+  }
+  for (int j = 0; j < c->n_res; ++j) {
+    if (c->res_kernels[j] <= 0) return fail(HFG_EINVAL, "resblock kernel %d must be > 0", j);
+    if (c->n_dil[j] <= 0 || c->n_dil[j] > HFG_MAX_DIL)
+      return fail(HFG_EINVAL, "resblock %d dilation count out of range", j);
+    for (int m = 0; m < c->n_dil[j]; ++m)
+      if (c->dil[j][m] <= 0) return fail(HFG_EINVAL, "dilation must be > 0");
+  }
+  return HFG_OK;
+}
+
+void add_param(hfg_handle* h, const std::string& key, std::vector<int64_t> shape) {
+  Param p;
+  p.shape = std::move(shape);
+  h->params[key] = std::move(p);
+  h->param_order.push_back(key);
+}
+
+int add_conv(hfg_handle* h, LayerKind kind, const std::string& mod, int cin, int cout, int k,
+             int dil, int pad) {
+  Layer L{};
+  L.kind = kind;
+  L.mod = mod;
+  L.C_in = cin;
+  L.C_out = cout;
+  L.k = k;
+  L.dil = dil;
+  L.pad = pad;
+  L.M = cout;
+  L.KT = k;
+  h->layers.push_back(L);
+  add_param(h, mod + ".weight", {cout, cin, k});
+  add_param(h, mod + ".bias", {cout});
+  return (int)h->layers.size() - 1;
+}
+
+// Build the layer list in the order of HiFiGANGenerator.__init__ (models/hifigan.py:177-222).
+void build_layers(hfg_handle* h) {
+  const hfg_config& c = h->cfg;
+  h->conv_pre = add_conv(h, L_CONV, "conv_pre", c.n_mels, c.c0, 7, 1, 3);
+  std::vector<int> ups_idx;
+  for (int i = 0; i < c.n_up; ++i) {
+    const int cin = c.c0 >> i, cout = c.c0 >> (i + 1);
+    const int u = c.up_rates[i], k = c.up_kernels[i];
+    Layer L{};
+    L.kind = L_UPS;
+    L.mod = "ups." + std::to_string(i);
+    L.C_in = cin;
+    L.C_out = cout;
+    L.k = k;
+    L.dil = 1;
+    L.s = u;
+    L.p = (k - u) / 2;  // models/hifigan.py:201 — Python floor division
+    if (k - u < 0 && (k - u) % 2 != 0) L.p -= 1;
+    L.M = cout * u;
+    L.KT = (k + u - 1) / u;  // taps per output phase
+    h->layers.push_back(L);
+    ups_idx.push_back((int)h->layers.size() - 1);
+    add_param(h, L.mod + ".weight", {cin, cout, k});
+    add_param(h, L.mod + ".bias", {cout});
+  }
+  for (int i = 0; i < c.n_up; ++i) {
+    const int ch = c.c0 >> (i + 1);
+    Stage st;
+    st.conv_ups = ups_idx[i];
+    for (int j = 0; j < c.n_res; ++j) {
+      const int kr = c.res_kernels[j];
+      const std::string pre = "mrfs." + std::to_string(i) + ".resblocks." + std::to_string(j);
+      for (int m = 0; m < c.n_dil[j]; ++m)
+        st.conv1.push_back(add_conv(h, L_CONV, pre + ".convs1." + std::to_string(m), ch, ch, kr,
+                                    c.dil[j][m], get_padding(kr, c.dil[j][m])));
+      for (int m = 0; m < c.n_dil[j]; ++m)
+        st.conv2.push_back(add_conv(h, L_CONV, pre + ".convs2." + std::to_string(m), ch, ch, kr, 1,
+                                    get_padding(kr, 1)));
+    }
+    h->stages.push_back(std::move(st));
+  }
+  h->conv_post = add_conv(h, L_POST, "conv_post", c.c0 >> c.n_up, 1, 7, 1, 3);
+
+  // GEMM tiling and packed-buffer offsets
+  size_t off = 0;
+  for (auto& L : h->layers) {
+    if (L.kind == L_POST) {
+      L.w_off = off;
+      L.w_len = (size_t)L.C_in * 7;
+      off += (L.w_len + 63) & ~(size_t)63;
+      L.b_off = off;
+      L.b_len = 1;
+      off += 64;
+      continue;
+    }
+    L.tile = hfg::tile_for_rows(L.M);
+    const TileCfg& t = kTiles[L.tile];
+    L.m_tiles = (L.M + t.MT() - 1) / t.MT();
+    L.n_chunks = (L.C_in + t.CK - 1) / t.CK;
+    L.w_off = off;
+    L.w_len = (size_t)L.m_tiles * L.n_chunks * t.MT() * t.CK * L.KT;
+    off += (L.w_len + 63) & ~(size_t)63;
+    L.b_off = off;
+    L.b_len = (size_t)L.m_tiles * t.MT();
+    off += (L.b_len + 63) & ~(size_t)63;
+  }
+  h->packed_host.assign(off, 0.f);
+}
+
+// Fragment order of conv1d_mfma_f32's A operand (see conv_kernels.hip):
+//   idx = ((((mt*n_chunks + c)*KT + j)*KK + kk)*WAVES_M + wave_m)*64*WM + lane*WM + wm
+//   row = mt*MT + wave_m*32*WM + wm*32 + (lane & 31),  ci = c*CK + 2*kk + (lane >> 5)
+// wt(row, ci, j) is the GEMM weight; zero outside [0,M) x [0,C_in).
+template <typename F>
+void pack_gemm_weights(const Layer& L, F wt, float* dst) {
+  const TileCfg& t = kTiles[L.tile];
+  const int KK = t.CK / 2;
+  size_t idx = 0;
+  for (int mt = 0; mt < L.m_tiles; ++mt)
+    for (int c = 0; c < L.n_chunks; ++c)
+      for (int j = 0; j < L.KT; ++j)
+        for (int kk = 0; kk < KK; ++kk)
+          for (int wave_m = 0; wave_m < t.WAVES_M; ++wave_m)
+            for (int lane = 0; lane < 64; ++lane)
+              for (int wm = 0; wm < t.WM; ++wm) {
+                const int row = mt * t.MT() + wave_m * 32 * t.WM + wm * 32 + (lane & 31);
+                const int ci = c * t.CK + 2 * kk + (lane >> 5);
+                dst[idx++] = (row < L.M && ci < L.C_in) ? wt(row, ci, j) : 0.f;
+              }
+}
+
+void pack_layer(hfg_handle* h, const Layer& L) {
+  const Param& W = h->params[L.mod + ".weight"];
+  const Param& Bp = h->params[L.mod + ".bias"];
+  float* dst = h->packed_host.data() + L.w_off;
+  float* bdst = h->packed_host.data() + L.b_off;
+  const float* w = W.data.data();
+  if (L.kind == L_POST) {
+    std::memcpy(dst, w, sizeof(float) * L.C_in * 7);  // [1][C][7]
+    bdst[0] = Bp.data[0];
+    return;
+  }
+  if (L.kind == L_CONV) {
+    const int cin = L.C_in, k = L.k;
+    // nn.Conv1d weight [C_out][C_in][k]
+    pack_gemm_weights(L, [&](int row, int ci, int j) { return w[((size_t)row * cin + ci) * k + j]; },
+                      dst);
+    for (size_t m = 0; m < L.b_len; ++m) bdst[m] = m < (size_t)L.M ? Bp.data[m] : 0.f;
+    return;
+  }
+  // L_UPS: polyphase ConvTranspose1d.  GEMM row m = co*s + r; tap jj reads
+  // x[u - (Q-1) + jj], i.e. original kernel index r + s*(Q-1-jj).
+  const int s = L.s, Q = L.KT, k = L.k, cout = L.C_out;
+  pack_gemm_weights(L,
+                    [&](int row, int ci, int jj) {
+                      const int co = row / s, r = row % s;
+                      const int kidx = r + s * (Q - 1 - jj);
+                      if (kidx >= k) return 0.f;
+                      // nn.ConvTranspose1d weight [C_in][C_out][k]
+                      return w[((size_t)ci * cout + co) * k + kidx];
+                    },
+                    dst);
+  for (size_t m = 0; m < L.b_len; ++m) bdst[m] = m < (size_t)L.M ? Bp.data[m / s] : 0.f;
+}
+
+int do_commit(hfg_handle* h) {
+  for (auto& key : h->param_order)
+    if (!h->params[key].set) return fail(HFG_EAGAIN, "weight '%s' was never set", key.c_str());
+  std::fill(h->packed_host.begin(), h->packed_host.end(), 0.f);
+  for (auto& L : h->layers) pack_layer(h, L);
+  if (h->device >= 0) {
+    DeviceGuard g(h->device);
+    if (!g.ok) return fail(HFG_ENODEV, "hipSetDevice(%d) failed", h->device);
+    // a previous forward may still read the old weights
+    hipError_t se = hipDeviceSynchronize();
+    if (se != hipSuccess) return hip_fail(se, "hipDeviceSynchronize(commit)");
+    if (h->packed_dev_len < h->packed_host.size()) {
+      if (h->packed_dev) (void)hipFree(h->packed_dev);
+      h->packed_dev = nullptr;
+      h->packed_dev_len = 0;
+      hipError_t e = hipMalloc(&h->packed_dev, sizeof(float) * h->packed_host.size());
+      if (e != hipSuccess) return fail(HFG_ENOMEM, "hipMalloc(weights): %s", hipGetErrorString(e));
+      h->packed_dev_len = h->packed_host.size();
+    }
+    hipError_t e = hipMemcpy(h->packed_dev, h->packed_host.data(),
+                             sizeof(float) * h->packed_host.size(), hipMemcpyHostToDevice);
+    if (e != hipSuccess) return hip_fail(e, "hipMemcpy(weights)");
+  }
+  h->dirty = false;
+  return HFG_OK;
+}
+
+// ---- shape bookkeeping ------------------------------------------------------
+struct Shapes {
+  std::vector<int64_t> L;  // L[0] = T, L[i+1] = length after stage i
+  int64_t buf_elems;       // per-buffer elements (all B items)
+};
+
+Shapes shapes_for(const hfg_handle* h, int64_t B, int64_t T) {
+  Shapes s;
+  s.L.push_back(T);
+  int64_t mx = (int64_t)h->cfg.c0 * T;
+  for (int i = 0; i < h->cfg.n_up; ++i) {
+    const int u = h->cfg.up_rates[i], k = h->cfg.up_kernels[i];
+    int p = (k - u) / 2;
+    if (k - u < 0 && (k - u) % 2 != 0) p -= 1;
+    const int64_t lo = (s.L.back() - 1) * u - 2 * p + k;
+    s.L.push_back(lo);
+    mx = std::max(mx, (int64_t)(h->cfg.c0 >> (i + 1)) * std::max<int64_t>(lo, 0));
+  }
+  s.buf_elems = ((mx * B + 63) / 64) * 64;
+  return s;
+}
+
+size_t ws_bytes_for(const hfg_handle* h, int64_t B, int64_t T) {
+  return 4 * sizeof(float) * (size_t)shapes_for(h, B, T).buf_elems;
+}
+
+hipEvent_t pool_event(hfg_handle* h) {
+  if (!h->event_pool.empty()) {
+    hipEvent_t e = h->event_pool.back();
+    h->event_pool.pop_back();
+    return e;
+  }
+  hipEvent_t e = nullptr;
+  if (hipEventCreate(&e) != hipSuccess) return nullptr;
+  return e;
+}
+
+void recycle_prof(hfg_handle* h) {
+  for (auto& r : h->prof) {
+    if (r.e0) h->event_pool.push_back(r.e0);
+    if (r.e1) h->event_pool.push_back(r.e1);
+  }
+  h->prof.clear();
+}
+
+struct Launcher {
+  hfg_handle* h;
+  hipStream_t stream;
+  ProfRec* rec = nullptr;
+  void begin(double flop, double bytes) {
+    rec = nullptr;
+    if (!h->profiling) return;
+    ProfRec r{nullptr, flop, bytes, pool_event(h), pool_event(h)};
+    if (r.e0) (void)hipEventRecord(r.e0, stream);
+    h->prof.push_back(r);
+    rec = &h->prof.back();
+  }
+  void end(const char* label) {
+    if (!rec) return;
+    rec->label = label;
+    if (rec->e1) (void)hipEventRecord(rec->e1, stream);
+  }
+};
+
+// One conv-layer launch (regular Conv1d).
+int run_conv(hfg_handle* h, Launcher& ln, const Layer& L, const float* x, int64_t B, int64_t Lt,
+             float* y, bool act_in, bool act_out, const float* res, float* mrf, int mrf_mode,
+             float mrf_div) {
+  const TileCfg& t = kTiles[L.tile];
+  ConvParams p{};
+  p.x = x;
+  p.x_bs = (int64_t)L.C_in * Lt;
+  p.C_in = L.C_in;
+  p.L_in = (int)Lt;
+  p.w = h->packed_dev + L.w_off;
+  p.bias = h->packed_dev + L.b_off;
+  p.y = y;
+  p.y_bs = (int64_t)L.C_out * Lt;
+  p.M = L.M;
+  p.N = (int)Lt;
+  p.off = -L.pad;
+  p.dil = L.dil;
+  p.kt = L.KT;
+  p.act_in = act_in;
+  p.act_out = act_out;
+  p.res = res;
+  p.mrf = mrf;
+  p.mrf_mode = mrf_mode;
+  p.mrf_div = mrf_div;
+  p.n_chunks = L.n_chunks;
+  const int n_tiles = (int)((Lt + t.NTILE() - 1) / t.NTILE());
+  const double flop = 2.0 * L.C_out * L.C_in * L.k * (double)Lt * B;
+  double bytes = 4.0 * B * Lt * (L.C_in + L.C_out) + 4.0 * L.C_out * L.C_in * L.k;
+  if (res) bytes += 4.0 * B * Lt * L.C_out;
+  if (mrf && (mrf_mode & 1)) bytes += 4.0 * B * Lt * L.C_out;
+  const char* name = nullptr;
+  ln.begin(flop, bytes);
+  hipError_t e = hfg::launch_conv((TileId)L.tile, L.KT, false, p, n_tiles, L.m_tiles, (int)B,
+                                  ln.stream, &name);
+  ln.end(name);
+  if (e != hipSuccess) return fail(HFG_EIO, "launch %s: %s", L.mod.c_str(), hipGetErrorString(e));
+  return HFG_OK;
+}
+
+int run_ups(hfg_handle* h, Launcher& ln, const Layer& L, const float* x, int64_t B, int64_t Lin,
+            int64_t Lout, float* y) {
+  const TileCfg& t = kTiles[L.tile];
+  ConvParams p{};
+  p.x = x;
+  p.x_bs = (int64_t)L.C_in * Lin;
+  p.C_in = L.C_in;
+  p.L_in = (int)Lin;
+  p.w = h->packed_dev + L.w_off;
+  p.bias = h->packed_dev + L.b_off;
+  p.y = y;
+  p.y_bs = (int64_t)L.C_out * Lout;
+  p.M = L.M;
+  // columns u: t_out + p = s*u + r  for t_out in [0, Lout)
+  p.N = (int)((Lout - 1 + L.p) / L.s + 1);
+  p.off = -(L.KT - 1);
+  p.dil = 1;
+  p.kt = L.KT;
+  p.act_in = 1;  // F.leaky_relu before every upsample, models/hifigan.py:244
+  p.act_out = 0;
+  p.ups_s = L.s;
+  p.ups_p = L.p;
+  p.L_out = (int)Lout;
+  p.n_chunks = L.n_chunks;
+  const int n_tiles = (p.N + t.NTILE() - 1) / t.NTILE();
+  const double flop = 2.0 * L.C_in * L.C_out * L.k * (double)Lin * B;
+  const double bytes = 4.0 * B * (L.C_in * Lin + L.C_out * Lout) + 4.0 * L.C_in * L.C_out * L.k;
+  const char* name = nullptr;
+  ln.begin(flop, bytes);
+  hipError_t e = hfg::launch_conv((TileId)L.tile, L.KT, true, p, n_tiles, L.m_tiles, (int)B,
+                                  ln.stream, &name);
+  ln.end(name);
+  if (e != hipSuccess) return fail(HFG_EIO, "launch %s: %s", L.mod.c_str(), hipGetErrorString(e));
+  return HFG_OK;
+}
+
+int forward_impl(hfg_handle* h, const float* mel, int64_t B, int64_t T, float* wav,
+                 int64_t out_len, void* ws, size_t ws_len, hipStream_t stream) {
+  if (!mel || !wav) return fail(HFG_EINVAL, "mel / wav pointer is NULL");
+  if (B <= 0 || T <= 0) return fail(HFG_EINVAL, "B and T must be > 0 (got %lld, %lld)",
+                                    (long long)B, (long long)T);
+  const Shapes sh = shapes_for(h, B, T);
+  for (auto l : sh.L)
+    if (l <= 0) return fail(HFG_EINVAL, "T=%lld gives an empty stage", (long long)T);
+  if (sh.L.back() != out_len)
+    return fail(HFG_EINVAL, "out_len %lld != expected %lld", (long long)out_len,
+                (long long)sh.L.back());
+  if ((double)sh.buf_elems / (double)B * 1.0 > 2147483647.0)
+    return fail(HFG_EINVAL, "per-item activation exceeds 2^31 elements");
+  if (ws_len < ws_bytes_for(h, B, T)) return fail(HFG_EINVAL, "workspace too small");
+  float* buf[4];
+  for (int i = 0; i < 4; ++i) buf[i] = reinterpret_cast<float*>(ws) + (size_t)i * sh.buf_elems;
+  float* X = buf[0];    // upsampled stage input
+  float* R = buf[1];    // running ResBlock state (also conv_pre output)
+  float* Tb = buf[2];   // conv1 output
+  float* MRF = buf[3];  // MRF accumulator
+  Launcher ln{h, stream};
+  const hfg_config& c = h->cfg;
+  int rc;
+  // conv_pre  (models/hifigan.py:238)
+  rc = run_conv(h, ln, h->layers[h->conv_pre], mel, B, T, R, false, false, nullptr, nullptr, 0,
+                1.f);
+  if (rc) return rc;
+  const float* cur = R;
+  for (int i = 0; i < c.n_up; ++i) {
+    const Stage& st = h->stages[i];
+    const int64_t Lin = sh.L[i], L = sh.L[i + 1];
+    // lrelu -> ups[i]  (models/hifigan.py:244-245)
+    rc = run_ups(h, ln, h->layers[st.conv_ups], cur, B, Lin, L, X);
+    if (rc) return rc;
+    // MRF (models/hifigan.py:116-131) of ResBlocks (:72-86)
+    int idx = 0;
+    for (int j = 0; j < c.n_res; ++j) {
+      for (int m = 0; m < c.n_dil[j]; ++m, ++idx) {
+        const float* src = (m == 0) ? X : R;
+        const Layer& L1 = h->layers[st.conv1[idx]];
+        const Layer& L2 = h->layers[st.conv2[idx]];
+        // xt = lrelu(conv1(lrelu(x)))
+        rc = run_conv(h, ln, L1, src, B, L, Tb, true, true, nullptr, nullptr, 0, 1.f);
+        if (rc) return rc;
+        const bool last = (m == c.n_dil[j] - 1);
+        if (!last) {
+          // x = x + conv2(xt)
+          rc = run_conv(h, ln, L2, Tb, B, L, R, false, false, src, nullptr, 0, 1.f);
+        } else {
+          int mode = (j > 0 ? 1 : 0) | (j == c.n_res - 1 ? 2 : 0);
+          rc = run_conv(h, ln, L2, Tb, B, L, nullptr, false, false, src, MRF, mode,
+                        (float)c.n_res);
+        }
+        if (rc) return rc;
+      }
+    }
+    cur = MRF;
+  }
+  // lrelu -> conv_post -> tanh  (models/hifigan.py:254-256)
+  {
+    const Layer& Lp = h->layers[h->conv_post];
+    const int64_t L = sh.L.back();
+    const char* name = nullptr;
+    ln.begin(2.0 * Lp.C_in * 7 * (double)L * B, 4.0 * B * L * (Lp.C_in + 1));
+    hipError_t e = hfg::launch_conv_post(cur, (int64_t)Lp.C_in * L, Lp.C_in, (int)L,
+                                         h->packed_dev + Lp.w_off, h->packed_dev + Lp.b_off, wav,
+                                         (int)B, stream, &name);
+    ln.end(name);
+    if (e != hipSuccess) return fail(HFG_EIO, "launch conv_post: %s", hipGetErrorString(e));
+  }
+  return HFG_OK;
+}
+
+}  // namespace
+
+// ============================================================================
+// C ABI
+// ============================================================================
+extern "C" {
+
+const char* hfg_version(void) { return "hifigan_hip 0.1.0 gfx950 fp32-mfma"; }
+
+const char* hfg_last_error(void) { return g_err.c_str(); }
+
+int hfg_create(const hfg_config* cfg, int device, hfg_handle** out) {
+  if (!out) return fail(HFG_EINVAL, "out is NULL");
+  *out = nullptr;
+  int rc = validate_config(cfg);
+  if (rc) return rc;
+  if (device >= 0) {
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess || n <= 0) return fail(HFG_ENODEV, "no HIP device available");
+    if (device >= n) return fail(HFG_ENODEV, "device %d out of range (%d devices)", device, n);
+  }
+  hfg_handle* h = new (std::nothrow) hfg_handle();
+  if (!h) return fail(HFG_ENOMEM, "out of host memory");
+  h->cfg = *cfg;
+  h->device = device;
+  build_layers(h);
+  *out = h;
+  return HFG_OK;
+}
+
+void hfg_destroy(hfg_handle* h) {
+  if (!h) return;
+  {
+    DeviceGuard g(h->device);
+    if (h->device >= 0) {
+      recycle_prof(h);
+      for (auto e : h->event_pool) (void)hipEventDestroy(e);
+      if (h->packed_dev) (void)hipFree(h->packed_dev);
+      if (h->ws) (void)hipFree(h->ws);
+    }
+  }
+  delete h;
+}
+
+int hfg_num_params(const hfg_handle* h) { return h ? (int)h->param_order.size() : 0; }
+
+int hfg_set_weight(hfg_handle* h, const char* name, const void* data, const int64_t* shape,
+                   int ndim, int is_device) {
+  if (!h || !name || !data || (!shape && ndim > 0))
+    return fail(HFG_EINVAL, "NULL argument to hfg_set_weight");
+  std::string key(name);
+  std::vector<int64_t> shp(shape, shape + ndim);
+  size_t n = 1;
+  for (auto d : shp) {
+    if (d < 0) return fail(HFG_EINVAL, "negative dimension for '%s'", name);
+    n *= (size_t)d;
+  }
+  std::vector<float> buf(n);
+  if (is_device) {
+    if (h->device < 0) return fail(HFG_EINVAL, "device pointer given to a host-only handle");
+    DeviceGuard g(h->device);
+    hipError_t e = hipMemcpy(buf.data(), data, n * sizeof(float), hipMemcpyDeviceToHost);
+    if (e != hipSuccess) return hip_fail(e, "hipMemcpy(set_weight)");
+  } else {
+    std::memcpy(buf.data(), data, n * sizeof(float));
+  }
+  auto ends_with = [&](const char* suf) {
+    size_t l = strlen(suf);
+    return key.size() > l && key.compare(key.size() - l, l, suf) == 0;
+  };
+  if (ends_with(".weight_g") || ends_with(".weight_v")) {
+    // apply_weight_norm layout (models/hifigan.py:274-283): w = g * v / ||v||, dim=0
+    const std::string mod = key.substr(0, key.size() - 9);
+    auto it = h->params.find(mod + ".weight");
+    if (it == h->params.end()) return fail(HFG_EINVAL, "unknown key '%s'", name);
+    const auto& wshape = it->second.shape;
+    if (ends_with(".weight_v")) {
+      if (shp != wshape) return fail(HFG_EINVAL, "shape mismatch for '%s'", name);
+    } else {
+      std::vector<int64_t> gshape(wshape.size(), 1);
+      gshape[0] = wshape[0];
+      if (shp != gshape) return fail(HFG_EINVAL, "shape mismatch for '%s'", name);
+    }
+    Param& part = h->wn_parts[key];
+    part.shape = shp;
+    part.data = std::move(buf);
+    part.set = true;
+    auto g = h->wn_parts.find(mod + ".weight_g");
+    auto v = h->wn_parts.find(mod + ".weight_v");
+    if (g != h->wn_parts.end() && v != h->wn_parts.end() && g->second.set && v->second.set) {
+      Param& W = it->second;
+      const size_t d0 = (size_t)wshape[0];
+      const size_t inner = v->second.data.size() / d0;
+      W.data.resize(v->second.data.size());
+      for (size_t i = 0; i < d0; ++i) {
+        double ss = 0.0;
+        const float* vv = v->second.data.data() + i * inner;
+        for (size_t q = 0; q < inner; ++q) ss += (double)vv[q] * vv[q];
+        const double scale = (double)g->second.data[i] / std::sqrt(ss);
+        for (size_t q = 0; q < inner; ++q) W.data[i * inner + q] = (float)(vv[q] * scale);
+      }
+      W.set = true;
+      h->dirty = true;
+    }
+    return HFG_OK;
+  }
+  auto it = h->params.find(key);
+  if (it == h->params.end()) return fail(HFG_EINVAL, "unknown key '%s'", name);
+  if (shp != it->second.shape) {
+    std::string want;
+    for (auto d : it->second.shape) want += std::to_string(d) + ",";
+    return fail(HFG_EINVAL, "shape mismatch for '%s' (expected [%s])", name, want.c_str());
+  }
+  it->second.data = std::move(buf);
+  it->second.set = true;
+  h->dirty = true;
+  return HFG_OK;
+}
+
+int hfg_commit_weights(hfg_handle* h) {
+  if (!h) return fail(HFG_EINVAL, "handle is NULL");
+  return do_commit(h);
+}
+
+int64_t hfg_out_len(const hfg_handle* h, int64_t T) {
+  if (!h || T <= 0) return -1;
+  return shapes_for(h, 1, T).L.back();
+}
+
+size_t hfg_workspace_bytes(const hfg_handle* h, int64_t B, int64_t T) {
+  if (!h || B <= 0 || T <= 0) return 0;
+  return ws_bytes_for(h, B, T);
+}
+
+int hfg_reserve(hfg_handle* h, int64_t B, int64_t T) {
+  if (!h) return fail(HFG_EINVAL, "handle is NULL");
+  if (h->device < 0) return fail(HFG_EINVAL, "host-only handle");
+  if (B <= 0 || T <= 0) return fail(HFG_EINVAL, "B and T must be > 0");
+  const size_t need = ws_bytes_for(h, B, T);
+  if (need <= h->ws_bytes) return HFG_OK;
+  DeviceGuard g(h->device);
+  if (!g.ok) return fail(HFG_ENODEV, "hipSetDevice(%d) failed", h->device);
+  if (h->ws) {
+    (void)hipDeviceSynchronize();
+    (void)hipFree(h->ws);
+  }
+  h->ws = nullptr;
+  h->ws_bytes = 0;
+  hipError_t e = hipMalloc(&h->ws, need);
+  if (e != hipSuccess) return fail(HFG_ENOMEM, "hipMalloc(workspace %zu B): %s", need,
+                                   hipGetErrorString(e));
+  h->ws_bytes = need;
+  return HFG_OK;
+}
+
+int hfg_forward_ws(hfg_handle* h, const float* mel, int64_t B, int64_t T, float* wav,
+                   int64_t out_len, void* workspace, size_t workspace_bytes, void* stream) {
+  if (!h) return fail(HFG_EINVAL, "handle is NULL");
+  if (h->device < 0) return fail(HFG_EINVAL, "host-only handle cannot run forward");
+  if (!workspace) return fail(HFG_EINVAL, "workspace is NULL");
+  DeviceGuard g(h->device);
+  if (!g.ok) return fail(HFG_ENODEV, "hipSetDevice(%d) failed", h->device);
+  if (h->dirty) {
+    int rc = do_commit(h);
+    if (rc) return rc;
+  }
+  return forward_impl(h, mel, B, T, wav, out_len, workspace, workspace_bytes,
+                      reinterpret_cast<hipStream_t>(stream));
+}
+
+int hfg_forward(hfg_handle* h, const float* mel, int64_t B, int64_t T, float* wav,
+                int64_t out_len, void* stream) {
+  if (!h) return fail(HFG_EINVAL, "handle is NULL");
+  if (h->device < 0) return fail(HFG_EINVAL, "host-only handle cannot run forward");
+  int rc = hfg_reserve(h, B, T);
+  if (rc) return rc;
+  return hfg_forward_ws(h, mel, B, T, wav, out_len, h->ws, h->ws_bytes, stream);
+}
+
+int hfg_set_profiling(hfg_handle* h, int enable) {
+  if (!h) return fail(HFG_EINVAL, "handle is NULL");
+  h->profiling = enable != 0;
+  return HFG_OK;
+}
+
+int hfg_profile_reset(hfg_handle* h) {
+  if (!h) return fail(HFG_EINVAL, "handle is NULL");
+  DeviceGuard g(h->device);
+  for (auto& r : h->prof)
+    if (r.e1) (void)hipEventSynchronize(r.e1);
+  recycle_prof(h);
+  return HFG_OK;
+}
+
+int hfg_profile_summary(hfg_handle* h, char* buf, size_t buflen) {
+  if (!h || !buf || buflen == 0) return fail(HFG_EINVAL, "bad arguments");
+  DeviceGuard g(h->device);
+  struct Agg {
+    int launches = 0;
+    double ms = 0, flop = 0, bytes = 0;
+  };
+  std::map<std::string, Agg> agg;
+  for (auto& r : h->prof) {
+    if (!r.e0 || !r.e1 || !r.label) continue;
+    hipError_t e = hipEventSynchronize(r.e1);
+    if (e != hipSuccess) return hip_fail(e, "hipEventSynchronize");
+    float ms = 0.f;
+    e = hipEventElapsedTime(&ms, r.e0, r.e1);
+    if (e != hipSuccess) return hip_fail(e, "hipEventElapsedTime");
+    Agg& a = agg[r.label];
+    a.launches++;
+    a.ms += ms;
+    a.flop += r.flop;
+    a.bytes += r.bytes;
+  }
+  std::string s = "{";
+  bool first = true;
+  for (auto& kv : agg) {
+    char line[512];
+    snprintf(line, sizeof(line), "%s\"%s\": {\"launches\": %d, \"ms\": %.6f, \"flop\": %.6e, "
+             "\"bytes\": %.6e}", first ? "" : ", ", kv.first.c_str(), kv.second.launches,
+             kv.second.ms, kv.second.flop, kv.second.bytes);
+    s += line;
+    first = false;
+  }
+  s += "}";
+  if (s.size() + 1 > buflen) return fail(HFG_EINVAL, "buffer too small (%zu needed)", s.size() + 1);
+  memcpy(buf, s.c_str(), s.size() + 1);
+  return HFG_OK;
+}
+
+// ---- inspection helpers (not part of the public header's compute API) ------
+// Copy the packed host image of layer `name` (module prefix) for host tests.
+int hfg_debug_packed_layer(hfg_handle* h, const char* mod, float* out, size_t cap,
+                           int64_t* info /* [8]: kind,M,KT,tile,m_tiles,n_chunks,w_len,b_len */) {
+  if (!h || !mod) return fail(HFG_EINVAL, "NULL argument");
+  for (auto& L : h->layers) {
+    if (L.mod != mod) continue;
+    if (info) {
+      info[0] = L.kind;
+      info[1] = L.M;
+      info[2] = L.KT;
+      info[3] = L.tile;
+      info[4] = L.m_tiles;
+      info[5] = L.n_chunks;
+      info[6] = (int64_t)L.w_len;
+      info[7] = (int64_t)L.b_len;
+    }
+    if (!out) return HFG_OK;
+    if (h->dirty) {
+      int rc = do_commit(h);
+      if (rc) return rc;
+    }
+    if (cap < L.w_len + L.b_len) return fail(HFG_EINVAL, "output buffer too small");
+    memcpy(out, h->packed_host.data() + L.w_off, sizeof(float) * L.w_len);
+    memcpy(out + L.w_len, h->packed_host.data() + L.b_off, sizeof(float) * L.b_len);
+    return HFG_OK;
+  }
+  return fail(HFG_EINVAL, "unknown layer '%s'", mod);
+}
+
+}  // extern "C"

@@ -1,0 +1,72 @@
+// kernels.h — device-kernel interface shared by the kernels (conv_kernels.hip)
+// and the host orchestration (hifigan_capi.cpp).  No torch types anywhere.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace hfg {
+
+constexpr float kLReluSlope = 0.1f;  // F.leaky_relu(x, 0.1), models/hifigan.py:81,83,244,254
+
+// One implicit-GEMM convolution launch:
+//   out[b][m][n] = bias[m] + sum_{ci, j} Wt[m][ci][j] * act_in(x[b][ci][n + off + j*dil])
+// with x zero outside [0, L_in).  Regular Conv1d: m = output channel.
+// Polyphase ConvTranspose1d (UPS): m = co*s + r and the result lands at
+// y[b][co][n*s + r - p].
+struct ConvParams {
+  const float* x;    // [B][C_in][L_in]
+  int64_t x_bs;      // batch stride of x (elements)
+  int C_in, L_in;
+  const float* w;    // packed weights (see pack layout in hifigan_capi.cpp)
+  const float* bias; // per GEMM row m, length >= m_tiles * MT
+  float* y;          // output [B][M][N] (regular) or [B][C_out][L_out] (UPS)
+  int64_t y_bs;
+  int M, N;          // GEMM rows (valid), output columns per batch item
+  int off, dil;      // input index = n + off + j*dil
+  int kt;            // taps (used when the kernel's KT template arg is 0)
+  int act_in;        // leaky_relu on the staged input
+  int act_out;       // leaky_relu on the output
+  const float* res;  // residual added to the output (same layout as y) or null
+  float* mrf;        // MRF accumulator; when set the result goes here, not to y
+  int mrf_mode;      // bit0: add existing mrf value, bit1: divide by mrf_div
+  float mrf_div;
+  int ups_s, ups_p, L_out;  // UPS store mapping
+  int n_chunks;      // ceil(C_in / CK)
+};
+
+// Tile configurations of conv1d_mfma_f32 (fp32 MFMA 32x32x2).
+//   MT = 32*WM*WAVES_M rows, NTILE = 32*WN*WAVES_N columns, CK input channels
+//   per LDS chunk, 64*WAVES_M*WAVES_N threads.
+struct TileCfg {
+  int WM, WN, WAVES_M, WAVES_N, CK;
+  constexpr int MT() const { return 32 * WM * WAVES_M; }
+  constexpr int NTILE() const { return 32 * WN * WAVES_N; }
+  constexpr int threads() const { return 64 * WAVES_M * WAVES_N; }
+};
+
+enum TileId { TILE_M128 = 0, TILE_M64 = 1, TILE_M32 = 2, TILE_COUNT = 3 };
+
+constexpr TileCfg kTiles[TILE_COUNT] = {
+    {2, 2, 2, 2, 8},  // M128: 128 x 128 tile, 4 waves of 64x64
+    {2, 2, 1, 4, 8},  // M64 :  64 x 256 tile, 4 waves of 64x64
+    {1, 4, 1, 4, 8},  // M32 :  32 x 512 tile, 4 waves of 32x128
+};
+
+inline TileId tile_for_rows(int M) {
+  if (M >= 128) return TILE_M128;
+  if (M >= 64) return TILE_M64;
+  return TILE_M32;
+}
+
+// Launch the conv kernel for (tile, taps, ups).  Returns a hipError_t and,
+// via *name, the kernel's template-instance name (as rocprofv3 prints it).
+hipError_t launch_conv(TileId tile, int kt, bool ups, const ConvParams& p, int n_tiles,
+                       int m_tiles, int batch, hipStream_t stream, const char** name);
+
+// conv_post + tanh: wav[b][t] = tanh(bias + sum_{c,j} w[c][j] * lrelu(x[b][c][t+j-3]))
+hipError_t launch_conv_post(const float* x, int64_t x_bs, int C, int L, const float* w,
+                            const float* bias, float* wav, int batch, hipStream_t stream,
+                            const char** name);
+
+}  // namespace hfg

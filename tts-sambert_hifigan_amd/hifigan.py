@@ -1,0 +1,273 @@
+"""Drop-in HiFi-GAN Generator for MI355X: the host-side mirror of the reference
+interface, running on the HIP kernels of libhifigan_hip.so.
+
+Mirrors ``models/hifigan.py`` of terrense/TTS-sambert_hifiGAN:
+
+* ``get_padding``          models/hifigan.py:21-23
+* ``ResBlock``             models/hifigan.py:26-86   (parameter container)
+* ``MRF``                  models/hifigan.py:89-131  (parameter container)
+* ``HiFiGANGenerator``     models/hifigan.py:134-283 (same ctor signature, same
+                           submodule tree ⇒ identical state_dict keys, same
+                           ``debug_shapes`` / ``DEBUG_SHAPES`` printing, same
+                           ``apply_weight_norm`` / ``remove_weight_norm``)
+* ``HiFiGAN``              models/hifigan.py:618-800, generation half
+                           (``forward`` / ``generate``); ``discriminate`` is
+                           GAN training and out of scope.
+
+``HiFiGANGenerator.forward`` hands ``mel.data_ptr()``, a workspace from torch's
+caching allocator and torch's current HIP stream to ``hfg_forward_ws``; the 78
+kernel launches run asynchronously on that stream.  The parameters live in the
+usual ``nn.Conv1d`` / ``nn.ConvTranspose1d`` containers (so ``state_dict`` /
+``load_state_dict`` are unchanged) and are re-packed into the kernels' layout
+whenever any of them changes.  Inference only: there is no CPU fallback and no
+autograd; a CPU input or an input that requires grad raises.
+"""
+from __future__ import annotations
+
+import os
+from typing import Dict, List, Tuple
+
+import torch
+import torch.nn as nn
+
+from . import _lib
+
+
+def get_padding(kernel_size: int, dilation: int = 1) -> int:
+    """Calculate padding to maintain sequence length (models/hifigan.py:21-23)."""
+    return int((kernel_size * dilation - dilation) / 2)
+
+
+class ResBlock(nn.Module):
+    """Parameter container with the reference layout (models/hifigan.py:34-70):
+    ``convs1[m]`` = Conv1d(C, C, k, dilation=d_m), ``convs2[m]`` = Conv1d(C, C, k).
+    Its computation runs inside the fused Generator schedule on the GPU."""
+
+    def __init__(self, channels: int, kernel_size: int = 3, dilation: Tuple[int, ...] = (1, 3, 5)):
+        super().__init__()
+        self.convs1 = nn.ModuleList()
+        self.convs2 = nn.ModuleList()
+        for d in dilation:
+            self.convs1.append(nn.Conv1d(channels, channels, kernel_size, stride=1, dilation=d,
+                                         padding=get_padding(kernel_size, d)))
+            self.convs2.append(nn.Conv1d(channels, channels, kernel_size, stride=1, dilation=1,
+                                         padding=get_padding(kernel_size, 1)))
+
+    def forward(self, x):
+        raise NotImplementedError(
+            "ResBlock runs only inside HiFiGANGenerator.forward on the HIP path")
+
+
+class MRF(nn.Module):
+    """Parameter container with the reference layout (models/hifigan.py:96-114)."""
+
+    def __init__(self, channels: int, resblock_kernel_sizes: List[int] = [3, 7, 11],
+                 resblock_dilation_sizes: List[List[int]] = [[1, 3, 5], [1, 3, 5], [1, 3, 5]]):
+        super().__init__()
+        self.resblocks = nn.ModuleList()
+        for kernel_size, dilations in zip(resblock_kernel_sizes, resblock_dilation_sizes):
+            self.resblocks.append(ResBlock(channels, kernel_size, tuple(dilations)))
+
+    def forward(self, x):
+        raise NotImplementedError("MRF runs only inside HiFiGANGenerator.forward on the HIP path")
+
+
+class HiFiGANGenerator(nn.Module):
+    """HiFi-GAN Generator, mel [B, n_mels, Tfrm] → wav [B, 1, T_wav] on MI355X.
+
+    Same constructor as models/hifigan.py:149-158.
+    """
+
+    def __init__(
+        self,
+        n_mels: int = 80,
+        upsample_rates: List[int] = [8, 8, 2, 2],
+        upsample_kernel_sizes: List[int] = [16, 16, 4, 4],
+        upsample_initial_channel: int = 512,
+        resblock_kernel_sizes: List[int] = [3, 7, 11],
+        resblock_dilation_sizes: List[List[int]] = [[1, 3, 5], [1, 3, 5], [1, 3, 5]],
+        debug_shapes: bool = False,
+    ):
+        super().__init__()
+        self.n_mels = n_mels
+        self.num_kernels = len(resblock_kernel_sizes)
+        self.num_upsamples = len(upsample_rates)
+        self.debug_shapes = debug_shapes or os.getenv("DEBUG_SHAPES", "0") == "1"
+
+        self.conv_pre = nn.Conv1d(n_mels, upsample_initial_channel, kernel_size=7, stride=1,
+                                  padding=3)
+        self.ups = nn.ModuleList()
+        self.mrfs = nn.ModuleList()
+        for i, (u, k) in enumerate(zip(upsample_rates, upsample_kernel_sizes)):
+            in_channels = upsample_initial_channel // (2 ** i)
+            out_channels = upsample_initial_channel // (2 ** (i + 1))
+            self.ups.append(nn.ConvTranspose1d(in_channels, out_channels, kernel_size=k, stride=u,
+                                               padding=(k - u) // 2))
+            self.mrfs.append(MRF(out_channels, resblock_kernel_sizes, resblock_dilation_sizes))
+        final_channels = upsample_initial_channel // (2 ** self.num_upsamples)
+        self.conv_post = nn.Conv1d(final_channels, 1, kernel_size=7, stride=1, padding=3)
+
+        self._hfg_cfg = _lib.make_config(n_mels, upsample_rates, upsample_kernel_sizes,
+                                         upsample_initial_channel, resblock_kernel_sizes,
+                                         resblock_dilation_sizes)
+        self._hfg_handles: Dict[int, _lib.Handle] = {}
+        self._hfg_fingerprint: Dict[int, tuple] = {}
+
+    # ------------------------------------------------------------------
+    def _weight_tensors(self):
+        """(state_dict-style key, tensor) of every parameter the kernels need,
+        with weight_g / weight_v passed through for weight-normed modules."""
+        for name, mod in self.named_modules():
+            if not isinstance(mod, (nn.Conv1d, nn.ConvTranspose1d)):
+                continue
+            if hasattr(mod, "weight_g") and hasattr(mod, "weight_v"):
+                yield name + ".weight_g", mod.weight_g
+                yield name + ".weight_v", mod.weight_v
+            else:
+                yield name + ".weight", mod.weight
+            yield name + ".bias", mod.bias
+
+    def _handle_for(self, device: torch.device) -> _lib.Handle:
+        idx = device.index if device.index is not None else torch.cuda.current_device()
+        h = self._hfg_handles.get(idx)
+        if h is None:
+            h = _lib.Handle(self._hfg_cfg, idx)
+            self._hfg_handles[idx] = h
+        tensors = list(self._weight_tensors())
+        fp = tuple((k, t.data_ptr(), t._version, tuple(t.shape)) for k, t in tensors)
+        if self._hfg_fingerprint.get(idx) != fp:
+            for k, t in tensors:
+                h.set_weight(k, t)
+            h.commit()
+            self._hfg_fingerprint[idx] = fp
+        return h
+
+    def hip_handle(self, device=None) -> _lib.Handle:
+        """The C-ABI handle for ``device`` with the current weights committed."""
+        if device is None:
+            device = torch.device("cuda", torch.cuda.current_device())
+        return self._handle_for(torch.device(device))
+
+    def output_length(self, t: int) -> int:
+        length = t
+        for u, k in zip(self._hfg_cfg.up_rates[: self.num_upsamples],
+                        self._hfg_cfg.up_kernels[: self.num_upsamples]):
+            length = (length - 1) * u - 2 * ((k - u) // 2) + k
+        return length
+
+    # ------------------------------------------------------------------
+    def forward(self, mel: torch.Tensor) -> torch.Tensor:
+        """Generate waveform from mel-spectrogram (models/hifigan.py:224-261).
+
+        Args:
+            mel: [B, n_mels, Tfrm] float32 on a HIP device
+        Returns:
+            wav: [B, 1, T_wav] float32, T_wav = Tfrm * prod(upsample_rates)
+        """
+        if self.debug_shapes:
+            print(f"[HiFiGANGenerator] Input mel shape: {mel.shape}")
+        if not isinstance(mel, torch.Tensor) or mel.dim() != 3:
+            raise RuntimeError(f"expected mel [B, n_mels, T], got {getattr(mel, 'shape', type(mel))}")
+        if mel.shape[1] != self.n_mels:
+            raise RuntimeError(f"expected {self.n_mels} mel channels, got {mel.shape[1]}")
+        if not mel.is_cuda:
+            raise RuntimeError("HiFiGANGenerator (MI355X) runs on the HIP device only; "
+                               "move the mel to 'cuda' (there is no CPU fallback)")
+        if torch.is_grad_enabled() and mel.requires_grad:
+            raise NotImplementedError("inference-only HIP path: no autograd through the Generator")
+        B, _, T = mel.shape
+        if B == 0 or T == 0:
+            raise RuntimeError("empty mel input")
+        mel_c = mel.detach().to(torch.float32).contiguous()
+        with torch.cuda.device(mel.device):
+            h = self._handle_for(mel.device)
+            out_len = h.out_len(T)
+            wav = torch.empty((B, 1, out_len), dtype=torch.float32, device=mel.device)
+            ws_bytes = h.workspace_bytes(B, T)
+            ws = torch.empty(ws_bytes, dtype=torch.uint8, device=mel.device)
+            stream = torch.cuda.current_stream(mel.device).cuda_stream
+            h.forward_ws(mel_c.data_ptr(), B, T, wav.data_ptr(), out_len, ws.data_ptr(), ws_bytes,
+                         stream)
+        if self.debug_shapes:
+            x_len = T
+            c = self.conv_pre.out_channels
+            print(f"[HiFiGANGenerator] After conv_pre: {torch.Size([B, c, x_len])}")
+            for i, up in enumerate(self.ups):
+                u, k = up.stride[0], up.kernel_size[0]
+                x_len = (x_len - 1) * u - 2 * ((k - u) // 2) + k
+                c = up.out_channels
+                print(f"[HiFiGANGenerator] After upsample {i}: {torch.Size([B, c, x_len])}")
+                print(f"[HiFiGANGenerator] After MRF {i}: {torch.Size([B, c, x_len])}")
+            print(f"[HiFiGANGenerator] Output wav shape: {wav.shape}")
+        return wav
+
+    def remove_weight_norm(self):
+        """models/hifigan.py:263-272"""
+        for layer in self.ups:
+            nn.utils.remove_weight_norm(layer)
+        for mrf in self.mrfs:
+            for resblock in mrf.resblocks:
+                for conv in resblock.convs1:
+                    nn.utils.remove_weight_norm(conv)
+                for conv in resblock.convs2:
+                    nn.utils.remove_weight_norm(conv)
+
+    def apply_weight_norm(self):
+        """models/hifigan.py:274-283 (the kernels fold g·v/||v|| at commit)."""
+        for layer in self.ups:
+            nn.utils.weight_norm(layer)
+        for mrf in self.mrfs:
+            for resblock in mrf.resblocks:
+                for conv in resblock.convs1:
+                    nn.utils.weight_norm(conv)
+                for conv in resblock.convs2:
+                    nn.utils.weight_norm(conv)
+
+
+class HiFiGAN(nn.Module):
+    """Generation half of the reference ``HiFiGAN`` wrapper (models/hifigan.py:618-800).
+
+    Accepts the reference constructor arguments; the discriminator arguments
+    are accepted and ignored because ``discriminate`` (GAN training) is out of
+    scope for this inference path.
+    """
+
+    def __init__(self, n_mels: int = 80, upsample_rates: List[int] = [8, 8, 2, 2],
+                 upsample_kernel_sizes: List[int] = [16, 16, 4, 4],
+                 upsample_initial_channel: int = 512,
+                 resblock_kernel_sizes: List[int] = [3, 7, 11],
+                 resblock_dilation_sizes: List[List[int]] = [[1, 3, 5], [1, 3, 5], [1, 3, 5]],
+                 msd_use_spectral_norm: bool = False, mpd_periods: List[int] = [2, 3, 5, 7, 11],
+                 mpd_use_spectral_norm: bool = False, debug_shapes: bool = False):
+        super().__init__()
+        self.debug_shapes = debug_shapes or os.getenv("DEBUG_SHAPES", "0") == "1"
+        self.generator = HiFiGANGenerator(
+            n_mels=n_mels, upsample_rates=upsample_rates,
+            upsample_kernel_sizes=upsample_kernel_sizes,
+            upsample_initial_channel=upsample_initial_channel,
+            resblock_kernel_sizes=resblock_kernel_sizes,
+            resblock_dilation_sizes=resblock_dilation_sizes, debug_shapes=debug_shapes)
+        self.msd = None
+        self.mpd = None
+
+    def forward(self, mel: torch.Tensor) -> torch.Tensor:
+        """models/hifigan.py:704-724"""
+        if self.debug_shapes:
+            print(f"[HiFiGAN] forward() - Input mel shape: {mel.shape}")
+        wav = self.generator(mel)
+        if self.debug_shapes:
+            print(f"[HiFiGAN] forward() - Output wav shape: {wav.shape}")
+        return wav
+
+    def generate(self, mel: torch.Tensor) -> torch.Tensor:
+        """models/hifigan.py:790-800"""
+        return self.forward(mel)
+
+    def discriminate(self, wav_real, wav_fake):
+        raise NotImplementedError("discriminators are GAN-training only; out of scope for the "
+                                  "MI355X inference path")
+
+    def load_state_dict(self, state_dict, strict: bool = True, assign: bool = False):
+        """Accepts a full reference HiFiGAN state_dict: msd.* / mpd.* keys are dropped."""
+        sd = {k: v for k, v in state_dict.items() if not k.startswith(("msd.", "mpd."))}
+        return super().load_state_dict(sd, strict=strict, assign=assign)
