@@ -1,0 +1,242 @@
+"""Benchmark of the MI355X HiFi-GAN Generator hot path (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--preset v1] [--batch 8] [--frames 1024]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N --steps K --warmup W
+
+A step = one Generator forward of a [batch, 80, frames] synthetic mel per GPU
+(default batch 8 × 1024 frames = BASELINE config 2; 8 GPUs × 8 = config 3),
+mel and weights resident in HBM before the timed region.  Utterances are
+sharded over ranks (weak scaling); weights are generated on rank 0 and
+broadcast once with RCCL.  Rank 0 prints ONE JSON line.
+
+Roofline: every kernel launch in the timed region is bracketed by HIP events
+recorded on the launch stream (libhifigan_hip profiling mode); the dominant
+kernel's achieved TFLOP/s = its algorithmic FLOP ÷ its summed launch time.
+cpu_baseline: the oracle's PyTorch-CPU restatement (same ATen ops as the
+reference) on this host's cores, rank 0 / N=1 only, on a bounded sample.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import __graft_entry__ as ge  # noqa: E402
+
+METRIC = ("audio samples/sec/GPU (HiFi-GAN 80-mel→22.05 kHz) at 1/2/4/8 MI355X; RTF")
+SAMPLE_RATE = 22050
+PEAK_FP32_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 matrix (= vector) peak
+PEAK_HBM_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--preset", default="v1", choices=["v1", "v2star"])
+    ap.add_argument("--batch", type=int, default=8, help="utterances per GPU")
+    ap.add_argument("--frames", type=int, default=1024)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-budget-s", type=float, default=12.0)
+    ap.add_argument("--no-profile", action="store_true",
+                    help="do not bracket launches with HIP events (no roofline)")
+    return ap.parse_args()
+
+
+def cpu_baseline(cfg, sd, frames, budget_s):
+    """Oracle (PyTorch-CPU restatement) on host cores: best of N runs of one
+    [1, 80, frames] utterance after a warm-up, within ~budget_s seconds."""
+    from oracle import hifigan_torch, prng
+    threads = torch.get_num_threads()
+    tsd = hifigan_torch.to_torch_state(sd)
+    mel = torch.from_numpy(prng.mel_input(1234, (1, cfg.n_mels, frames)))
+    hifigan_torch.generator_forward(tsd, cfg, mel[:, :, :32])  # warm-up
+    best, runs, t_all = None, 0, time.perf_counter()
+    while runs < 1 or (time.perf_counter() - t_all < budget_s and runs < 3):
+        t0 = time.perf_counter()
+        wav = hifigan_torch.generator_forward(tsd, cfg, mel)
+        dt = time.perf_counter() - t0
+        best = dt if best is None else min(best, dt)
+        runs += 1
+    samples = wav.shape[-1]
+    return {"value": samples / best, "unit": "audio samples/s", "cores": threads,
+            "kind": "port",
+            "sample": f"1 utterance [1,{cfg.n_mels},{frames}] of the bench workload, best of {runs} "
+                      f"after warm-up, oracle/hifigan_torch.py (same ATen ops as the reference), "
+                      f"{threads} threads, {os.cpu_count()} host CPUs visible",
+            "rtf": best / (samples / SAMPLE_RATE)}
+
+
+def main():
+    args = parse()
+    rank, world, local_rank = 0, 1, 0
+    if "RANK" in os.environ and int(os.environ.get("WORLD_SIZE", "1")) > 1:
+        rank, world, local_rank = (int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"]),
+                                   int(os.environ.get("LOCAL_RANK", "0")))
+    if world != args.gpus and rank == 0:
+        print(f"[bench] note: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+    assert torch.cuda.is_available(), "bench.py needs MI355X GPUs"
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    pkg = ge.load_package()
+    pkg.load_library()
+    import importlib
+    hdist = importlib.import_module(ge.PKG_NAME + ".dist")
+    from oracle import config as C, prng  # weight / input generators (test infrastructure)
+
+    cfg = C.PRESETS[args.preset]
+    spec = [(k, s) for k, s, _ in C.param_specs(cfg)]
+    sd_np = C.make_state_dict(cfg, seed=0) if rank == 0 else None
+    if world > 1:
+        sd = hdist.broadcast_state_dict({k: torch.from_numpy(v) for k, v in sd_np.items()}
+                                        if rank == 0 else None, spec, dev, src=0)
+    else:
+        sd = {k: torch.from_numpy(v) for k, v in sd_np.items()}
+    gen = pkg.HiFiGANGenerator(**cfg.kwargs()).eval()
+    gen.load_state_dict({k: v.detach().cpu() for k, v in sd.items()})
+    h = gen.hip_handle(dev)
+
+    # this rank's utterances of the global batch (weak scaling: batch per GPU fixed)
+    global_batch = args.batch * world
+    start, stop = hdist.shard_range(global_batch, world, rank)
+    B, T = stop - start, args.frames
+    gmel = torch.Generator().manual_seed(1234)
+    mel_all = torch.randn(global_batch, cfg.n_mels, T, generator=gmel)
+    mel = mel_all[start:stop].contiguous().to(dev)
+    out_len = h.out_len(T)
+    wav = torch.empty((B, 1, out_len), dtype=torch.float32, device=dev)
+    ws_bytes = h.workspace_bytes(B, T)
+    ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
+    stream = torch.cuda.current_stream(dev)
+
+    def step():
+        h.forward_ws(mel.data_ptr(), B, T, wav.data_ptr(), out_len, ws.data_ptr(), ws_bytes,
+                     stream.cuda_stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+
+    profile = not args.no_profile
+    if profile:
+        h.profile_reset()
+        h.set_profiling(True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        dist.barrier()
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    prof = {}
+    if profile:
+        h.set_profiling(False)
+        prof = h.profile_summary()
+
+    samples_total = global_batch * out_len * args.steps
+    value = samples_total / elapsed
+    ms_per_step = 1000.0 * elapsed / args.steps
+
+    if rank != 0:
+        if world > 1:
+            dist.destroy_process_group()
+        return
+
+    line = {
+        "metric": METRIC,
+        "value": value,
+        "unit": "audio samples/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": ms_per_step,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic: mel ~ N(0,1) (torch seed 1234), PRNG default-init V1 weights "
+                "(no checkpoint)",
+        "config": {
+            "workload": f"HiFi-GAN {args.preset.upper()} Generator forward, mel [{args.batch},"
+                        f"{cfg.n_mels},{T}] per GPU -> wav [{args.batch},1,{out_len}]",
+            "batch_per_gpu": args.batch,
+            "frames": T,
+            "global_batch": global_batch,
+            "parallelism": f"dp{world} (utterance-sharded, RCCL weight broadcast at init)",
+        },
+        "per_gpu": value / world,
+        "rtf": (elapsed / args.steps) / (args.batch * out_len / SAMPLE_RATE),
+    }
+    if prof:
+        tot_ms = sum(v["ms"] for v in prof.values()) / args.steps
+        dom_name, dom = max(prof.items(), key=lambda kv: kv[1]["ms"])
+        achieved = dom["flop"] / (dom["ms"] * 1e-3) / 1e12
+        traffic = None
+        pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+        if os.path.exists(pmc_path):
+            try:
+                pmc = json.load(open(pmc_path))
+                if dom_name in pmc and pmc[dom_name].get("bytes_per_launch"):
+                    traffic = pmc[dom_name]["bytes_per_launch"]
+            except Exception:
+                traffic = None
+        line["roofline"] = {
+            "bound": "mfma",
+            "kernel": dom_name,
+            "achieved": achieved,
+            "peak": PEAK_FP32_TFLOPS,
+            "unit": "TFLOP/s",
+            "frac": achieved / PEAK_FP32_TFLOPS,
+            "traffic": traffic,
+            "launches_per_step": dom["launches"] / args.steps,
+            "avg_launch_ms": dom["ms"] / dom["launches"],
+            "flop_per_launch": dom["flop"] / dom["launches"],
+            "alg_bytes_per_launch": dom["bytes"] / dom["launches"],
+            "share_of_step": dom["ms"] / args.steps / ms_per_step,
+        }
+        all_flop = sum(v["flop"] for v in prof.values()) / args.steps
+        all_bytes = sum(v["bytes"] for v in prof.values()) / args.steps
+        step_s = elapsed / args.steps
+        line["roofline_step"] = {
+            "compute_TFLOPs": all_flop / step_s / 1e12,
+            "compute_frac_fp32": all_flop / step_s / 1e12 / PEAK_FP32_TFLOPS,
+            "hbm_model_GBs": all_bytes / step_s / 1e9,
+            "hbm_model_frac": all_bytes / step_s / 1e9 / PEAK_HBM_GBS,
+            "kernel_time_ms": tot_ms,
+            "note": "algorithmic FLOP / layer-streaming bytes (SURVEY.md §8(d)) per step / step time",
+        }
+        line["kernels"] = {k: {"launches": v["launches"] // args.steps,
+                               "ms_per_step": v["ms"] / args.steps,
+                               "TFLOPs": v["flop"] / (v["ms"] * 1e-3) / 1e12 if v["ms"] else None}
+                           for k, v in sorted(prof.items(), key=lambda kv: -kv[1]["ms"])}
+    if world == 1 and not args.no_cpu_baseline:
+        cfg_np = C.make_state_dict(cfg, seed=0) if sd_np is None else sd_np
+        line["cpu_baseline"] = cpu_baseline(cfg, cfg_np, T, args.cpu_budget_s)
+        line["cpu_baseline"]["gpu_over_cpu"] = value / line["cpu_baseline"]["value"]
+    print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

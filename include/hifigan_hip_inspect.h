@@ -19,9 +19,9 @@ extern "C" {
 #endif
 
 /* Copy the packed image of one layer (module prefix, e.g. "ups.0") into out:
- * w_len packed GEMM weights followed by b_len per-row biases.  info[8]
+ * w_len packed GEMM weights followed by b_len per-row biases.  info[10]
  * receives {kind (0 conv, 1 ups, 2 post), M, KT, tile, m_tiles, n_chunks,
- * w_len, b_len}.  With out == NULL only info is filled. */
+ * w_len, b_len, CK, MT}.  With out == NULL only info is filled. */
 int hfg_debug_packed_layer(hfg_handle* h, const char* mod, float* out, size_t cap,
                            int64_t* info);
 

@@ -15,8 +15,8 @@ import torch.nn.functional as F
 from conftest import ROOT
 from oracle import config as C
 
-# kTiles of csrc/kernels.h: (WM, WN, WAVES_M, WAVES_N, CK)
-TILES = [(2, 2, 2, 2, 8), (2, 2, 1, 4, 8), (1, 4, 1, 4, 8)]
+# kTiles of csrc/kernels.h: (WM, WN, WAVES_M, WAVES_N)
+TILES = [(2, 2, 2, 2), (2, 2, 1, 4), (1, 4, 1, 4)]
 
 
 def header_symbols():
@@ -88,8 +88,10 @@ def test_set_weight_errors_and_commit(pkg):
 
 def unpack_gemm(info, packed, cin):
     """Invert the fragment order of conv_kernels.hip → Wt[row][ci][j]."""
-    WM, WN, WAVES_M, WAVES_N, CK = TILES[info["tile"]]
+    WM, WN, WAVES_M, WAVES_N = TILES[info["tile"]]
+    CK = info["CK"]
     MT = 32 * WM * WAVES_M
+    assert MT == info["MT"]
     KK = CK // 2
     KT = info["KT"]
     shape = (info["m_tiles"], info["n_chunks"], KT, KK, WAVES_M, 64, WM)

@@ -33,24 +33,30 @@
 namespace hfg {
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+typedef __attribute__((address_space(1))) void* gptr_t;
 
 __device__ __forceinline__ float lrelu(float v) { return v > 0.f ? v : v * kLReluSlope; }
 
 template <int KT_, int WM, int WN, int WAVES_M, int WAVES_N, int CK, bool UPS>
-__global__ void __launch_bounds__(64 * WAVES_M * WAVES_N)
+__global__ void __launch_bounds__(64 * WAVES_M * WAVES_N, 3)
 conv1d_mfma_f32(const ConvParams p) {
-  constexpr int NT = 64 * WAVES_M * WAVES_N;
+  constexpr int NW = WAVES_M * WAVES_N;
+  constexpr int NT = 64 * NW;
   constexpr int MT = 32 * WM * WAVES_M;
   constexpr int NTILE = 32 * WN * WAVES_N;
   constexpr int KK = CK / 2;
   static_assert(CK % 2 == 0, "CK must be even (K=2 per MFMA)");
+  // input-staging slots per thread (upper bound over the halos this instance accepts)
+  constexpr int XQ = (CK * (NTILE + halo_max(KT_)) + NT - 1) / NT;
   const int KT = KT_ > 0 ? KT_ : p.kt;
+  const int XW = NTILE + (KT - 1) * p.dil;
+  const int nx = CK * XW;
+  const float inv_xw = 1.0f / (float)XW;
+  const int wchunk = MT * CK * KT;            // floats per weight slab
+  const int stage_sz = wchunk + ((nx + 3) & ~3);
 
   extern __shared__ __attribute__((aligned(16))) float lds[];
-  const int wchunk = MT * CK * KT;
-  float* Ws = lds;
-  float* Xs = lds + wchunk;
-  const int XW = NTILE + (KT - 1) * p.dil;
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -62,6 +68,47 @@ conv1d_mfma_f32(const ConvParams p) {
   const int b = blockIdx.z;
   const float* __restrict__ xb = p.x + (int64_t)b * p.x_bs;
   const float* __restrict__ wsrc = p.w + (int64_t)mt * p.n_chunks * wchunk;
+  const int gbase = n0 + p.off;
+  const int half = lane >> 5;  // K index inside the MFMA (0/1)
+  const int col = lane & 31;   // GEMM column inside a 32-wide tile
+
+  // ---- weight slab: async global -> LDS copy (global_load_lds_dwordx4) ----
+  auto issue_w = [&](int c, float* Ws) {
+    const float* src = wsrc + (int64_t)c * wchunk;
+    const int n16 = wchunk >> 2;
+    for (int i = wave; i * 64 < n16; i += NW) {
+      const int piece = i * 64 + lane;
+      if (piece < n16)
+        __builtin_amdgcn_global_load_lds((gptr_t)(src + piece * 4), (lds_ptr_t)(Ws + i * 256), 16,
+                                         0, 0);
+    }
+  };
+  // ---- input rows: registers (zero padding, branch-free loads) ----
+  float xv[XQ];
+  auto load_x = [&](int c) {
+    const int ci0 = c * CK;
+#pragma unroll
+    for (int q = 0; q < XQ; ++q) {
+      const int i = tid + q * NT;
+      const int ci = (int)(((float)i + 0.5f) * inv_xw);
+      const int t = i - ci * XW;
+      const int gi = gbase + t;
+      const int cg = ci0 + ci;
+      const bool ok = (i < nx) && (cg < p.C_in) && ((unsigned)gi < (unsigned)p.L_in);
+      const int64_t idx = ok ? (int64_t)cg * p.L_in + gi : 0;
+      const float v = xb[idx];
+      xv[q] = ok ? v : 0.f;
+    }
+  };
+  auto store_x = [&](float* Xs) {
+#pragma unroll
+    for (int q = 0; q < XQ; ++q) {
+      const int i = tid + q * NT;
+      float v = xv[q];
+      if (p.act_in) v = lrelu(v);
+      if (i < nx) Xs[i] = v;
+    }
+  };
 
   floatx16 acc[WM][WN];
 #pragma unroll
@@ -71,68 +118,70 @@ conv1d_mfma_f32(const ConvParams p) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][k][r] = 0.f;
 
-  const int half = lane >> 5;     // K index inside the MFMA (0/1)
-  const int col = lane & 31;      // GEMM column inside a 32-wide tile
+  // fragment loads for MFMA step s = j*KK + kk of one stage
+  auto load_frag = [&](const float* Ws, const float* Xs, int j, int kk, float (&a)[WM],
+                       float (&bv)[WN]) {
+    const float* wa = Ws + ((j * KK + kk) * WAVES_M + wave_m) * 64 * WM + lane * WM;
+    if constexpr (WM == 2) {
+      const float2 a2 = *reinterpret_cast<const float2*>(wa);
+      a[0] = a2.x;
+      a[1] = a2.y;
+    } else {
+#pragma unroll
+      for (int i = 0; i < WM; ++i) a[i] = wa[i];
+    }
+    const float* xr = Xs + (2 * kk + half) * XW + wave_n * 32 * WN + col + j * p.dil;
+#pragma unroll
+    for (int k = 0; k < WN; ++k) bv[k] = xr[k * 32];
+  };
+  auto mma = [&](const float (&a)[WM], const float (&bv)[WN]) {
+#pragma unroll
+    for (int i = 0; i < WM; ++i)
+#pragma unroll
+      for (int k = 0; k < WN; ++k)
+        acc[i][k] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i], bv[k], acc[i][k], 0, 0, 0);
+  };
 
+  // ---- prologue: stage chunk 0 ----
+  issue_w(0, lds);
+  load_x(0);
+  store_x(lds + wchunk);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  // ---- main loop: compute chunk c from stage c&1 while chunk c+1 lands in the other ----
   for (int c = 0; c < p.n_chunks; ++c) {
-    // ---- stage the weight slab (fragment-ordered, contiguous) ----
-    {
-      const float4* __restrict__ s4 = reinterpret_cast<const float4*>(wsrc + (int64_t)c * wchunk);
-      float4* d4 = reinterpret_cast<float4*>(Ws);
-      const int n4 = wchunk >> 2;
-      for (int i = tid; i < n4; i += NT) d4[i] = s4[i];
+    float* Ws = lds + (c & 1) * stage_sz;
+    float* Xs = Ws + wchunk;
+    float* Wn = lds + ((c + 1) & 1) * stage_sz;
+    const bool has_next = c + 1 < p.n_chunks;
+    if (has_next) {
+      issue_w(c + 1, Wn);
+      load_x(c + 1);
     }
-    // ---- stage input rows with zero padding + pre-activation ----
-    {
-      const int ci0 = c * CK;
-      const int gbase = n0 + p.off;
+    if constexpr (KT_ > 0) {
+      constexpr int S = KT_ * KK;
+      float a0[WM], b0[WN], a1[WM], b1[WN];
+      load_frag(Ws, Xs, 0, 0, a0, b0);
 #pragma unroll
-      for (int ci = 0; ci < CK; ++ci) {
-        const int cg = ci0 + ci;
-        const bool row_ok = cg < p.C_in;
-        const float* __restrict__ xrow = xb + (int64_t)cg * p.L_in;
-        for (int t = tid; t < XW; t += NT) {
-          const int gi = gbase + t;
-          float v = 0.f;
-          if (row_ok && gi >= 0 && gi < p.L_in) {
-            v = xrow[gi];
-            if (p.act_in) v = lrelu(v);
-          }
-          Xs[ci * XW + t] = v;
+      for (int s = 0; s < S; s += 2) {
+        if (s + 1 < S) load_frag(Ws, Xs, (s + 1) / KK, (s + 1) % KK, a1, b1);
+        mma(a0, b0);
+        if (s + 2 < S) load_frag(Ws, Xs, (s + 2) / KK, (s + 2) % KK, a0, b0);
+        if (s + 1 < S) mma(a1, b1);
+      }
+    } else {
+      for (int j = 0; j < KT; ++j) {
+#pragma unroll
+        for (int kk = 0; kk < KK; ++kk) {
+          float a[WM], bv[WN];
+          load_frag(Ws, Xs, j, kk, a, bv);
+          mma(a, bv);
         }
       }
     }
-    __syncthreads();
-
-    const float* wa_base = Ws + wave_m * 64 * WM + lane * WM;
-    const float* xr_base = Xs + half * XW + wave_n * 32 * WN + col;
-    constexpr int KT_UNROLL = KT_ > 0 ? KT_ : 1;
-#pragma unroll KT_UNROLL
-    for (int j = 0; j < KT; ++j) {
-      const float* xr_j = xr_base + j * p.dil;
-#pragma unroll
-      for (int kk = 0; kk < KK; ++kk) {
-        const float* wa = wa_base + (j * KK + kk) * WAVES_M * 64 * WM;
-        float a[WM];
-        if constexpr (WM == 2) {
-          const float2 a2 = *reinterpret_cast<const float2*>(wa);
-          a[0] = a2.x;
-          a[1] = a2.y;
-        } else {
-#pragma unroll
-          for (int i = 0; i < WM; ++i) a[i] = wa[i];
-        }
-        const float* xr = xr_j + 2 * kk * XW;
-        float bv[WN];
-#pragma unroll
-        for (int k = 0; k < WN; ++k) bv[k] = xr[k * 32];
-#pragma unroll
-        for (int i = 0; i < WM; ++i)
-#pragma unroll
-          for (int k = 0; k < WN; ++k)
-            acc[i][k] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i], bv[k], acc[i][k], 0, 0, 0);
-      }
-    }
+    if (has_next) store_x(Wn + wchunk);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }
 
@@ -215,7 +264,9 @@ typedef void (*ConvFn)(const ConvParams);
 template <int KT, int TILE, bool UPS>
 struct Inst {
   static constexpr TileCfg t = kTiles[TILE];
-  static ConvFn fn() { return conv1d_mfma_f32<KT, t.WM, t.WN, t.WAVES_M, t.WAVES_N, t.CK, UPS>; }
+  static ConvFn fn() {
+    return conv1d_mfma_f32<KT, t.WM, t.WN, t.WAVES_M, t.WAVES_N, ck_for(KT, TILE), UPS>;
+  }
 };
 
 struct Entry {
@@ -230,14 +281,13 @@ struct Entry {
 #define HFG_ENTRY(KT, TILE, UPS) \
   { KT, TILE, UPS, Inst<KT, TILE, UPS>::fn(), false, {0} }
 
+#define HFG_ENTRIES_KT(KT, UPS) \
+  HFG_ENTRY(KT, 0, UPS), HFG_ENTRY(KT, 1, UPS), HFG_ENTRY(KT, 2, UPS)
+
 Entry g_entries[] = {
-    HFG_ENTRY(3, 0, false),  HFG_ENTRY(3, 1, false),  HFG_ENTRY(3, 2, false),
-    HFG_ENTRY(5, 0, false),  HFG_ENTRY(5, 1, false),  HFG_ENTRY(5, 2, false),
-    HFG_ENTRY(7, 0, false),  HFG_ENTRY(7, 1, false),  HFG_ENTRY(7, 2, false),
-    HFG_ENTRY(11, 0, false), HFG_ENTRY(11, 1, false), HFG_ENTRY(11, 2, false),
-    HFG_ENTRY(0, 0, false),  HFG_ENTRY(0, 1, false),  HFG_ENTRY(0, 2, false),
-    HFG_ENTRY(2, 0, true),   HFG_ENTRY(2, 1, true),   HFG_ENTRY(2, 2, true),
-    HFG_ENTRY(0, 0, true),   HFG_ENTRY(0, 1, true),   HFG_ENTRY(0, 2, true),
+    HFG_ENTRIES_KT(3, false), HFG_ENTRIES_KT(5, false), HFG_ENTRIES_KT(7, false),
+    HFG_ENTRIES_KT(11, false), HFG_ENTRIES_KT(2, false), HFG_ENTRIES_KT(0, false),
+    HFG_ENTRIES_KT(2, true),   HFG_ENTRIES_KT(3, true),  HFG_ENTRIES_KT(0, true),
 };
 
 }  // namespace
@@ -254,11 +304,14 @@ hipError_t launch_conv(TileId tile, int kt, bool ups, const ConvParams& p, int n
   if (!e) e = generic;
   if (!e) return hipErrorInvalidValue;
   const TileCfg& t = kTiles[tile];
+  const int ck = ck_for(e->kt, tile);
   if (!e->name[0])
     snprintf(e->name, sizeof(e->name), "conv1d_mfma_f32<%d, %d, %d, %d, %d, %d, %s>", e->kt, t.WM,
-             t.WN, t.WAVES_M, t.WAVES_N, t.CK, e->ups ? "true" : "false");
+             t.WN, t.WAVES_M, t.WAVES_N, ck, e->ups ? "true" : "false");
+  if ((kt - 1) * p.dil > halo_max(e->kt)) return hipErrorInvalidValue;
   const int xw = t.NTILE() + (kt - 1) * p.dil;
-  const size_t lds = sizeof(float) * ((size_t)t.MT() * t.CK * kt + (size_t)t.CK * xw);
+  const size_t stage = (size_t)t.MT() * ck * kt + (((size_t)ck * xw + 3) & ~(size_t)3);
+  const size_t lds = sizeof(float) * 2 * stage;
   if (lds > 160 * 1024) return hipErrorInvalidValue;
   if (lds > 64 * 1024 && !e->lds_attr_set) {
     hipError_t err = hipFuncSetAttribute(reinterpret_cast<const void*>(e->fn),

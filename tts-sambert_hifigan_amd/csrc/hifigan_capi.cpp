@@ -52,7 +52,7 @@ struct Layer {
   int C_in, C_out, k, dil, pad;
   int s, p;          // ConvTranspose1d stride / padding
   // GEMM view
-  int M, KT, tile, m_tiles, n_chunks;
+  int M, KT, CK, tile, m_tiles, n_chunks;
   size_t w_off, b_off;  // offsets (floats) into the packed device buffer
   size_t w_len, b_len;
 };
@@ -217,10 +217,11 @@ void build_layers(hfg_handle* h) {
     }
     L.tile = hfg::tile_for_rows(L.M);
     const TileCfg& t = kTiles[L.tile];
+    L.CK = hfg::ck_for(hfg::dispatch_kt(L.KT), L.tile);
     L.m_tiles = (L.M + t.MT() - 1) / t.MT();
-    L.n_chunks = (L.C_in + t.CK - 1) / t.CK;
+    L.n_chunks = (L.C_in + L.CK - 1) / L.CK;
     L.w_off = off;
-    L.w_len = (size_t)L.m_tiles * L.n_chunks * t.MT() * t.CK * L.KT;
+    L.w_len = (size_t)L.m_tiles * L.n_chunks * t.MT() * L.CK * L.KT;
     off += (L.w_len + 63) & ~(size_t)63;
     L.b_off = off;
     L.b_len = (size_t)L.m_tiles * t.MT();
@@ -236,7 +237,7 @@ void build_layers(hfg_handle* h) {
 template <typename F>
 void pack_gemm_weights(const Layer& L, F wt, float* dst) {
   const TileCfg& t = kTiles[L.tile];
-  const int KK = t.CK / 2;
+  const int KK = L.CK / 2;
   size_t idx = 0;
   for (int mt = 0; mt < L.m_tiles; ++mt)
     for (int c = 0; c < L.n_chunks; ++c)
@@ -246,7 +247,7 @@ void pack_gemm_weights(const Layer& L, F wt, float* dst) {
             for (int lane = 0; lane < 64; ++lane)
               for (int wm = 0; wm < t.WM; ++wm) {
                 const int row = mt * t.MT() + wave_m * 32 * t.WM + wm * 32 + (lane & 31);
-                const int ci = c * t.CK + 2 * kk + (lane >> 5);
+                const int ci = c * L.CK + 2 * kk + (lane >> 5);
                 dst[idx++] = (row < L.M && ci < L.C_in) ? wt(row, ci, j) : 0.f;
               }
 }
@@ -760,7 +761,7 @@ int hfg_profile_summary(hfg_handle* h, char* buf, size_t buflen) {
 // ---- inspection helpers (not part of the public header's compute API) ------
 // Copy the packed host image of layer `name` (module prefix) for host tests.
 int hfg_debug_packed_layer(hfg_handle* h, const char* mod, float* out, size_t cap,
-                           int64_t* info /* [8]: kind,M,KT,tile,m_tiles,n_chunks,w_len,b_len */) {
+                           int64_t* info) {
   if (!h || !mod) return fail(HFG_EINVAL, "NULL argument");
   for (auto& L : h->layers) {
     if (L.mod != mod) continue;
@@ -773,6 +774,8 @@ int hfg_debug_packed_layer(hfg_handle* h, const char* mod, float* out, size_t ca
       info[5] = L.n_chunks;
       info[6] = (int64_t)L.w_len;
       info[7] = (int64_t)L.b_len;
+      info[8] = L.CK;
+      info[9] = L.kind == L_POST ? 0 : kTiles[L.tile].MT();
     }
     if (!out) return HFG_OK;
     if (h->dirty) {

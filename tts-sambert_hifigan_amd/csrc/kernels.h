@@ -36,10 +36,10 @@ struct ConvParams {
 };
 
 // Tile configurations of conv1d_mfma_f32 (fp32 MFMA 32x32x2).
-//   MT = 32*WM*WAVES_M rows, NTILE = 32*WN*WAVES_N columns, CK input channels
-//   per LDS chunk, 64*WAVES_M*WAVES_N threads.
+//   MT = 32*WM*WAVES_M rows, NTILE = 32*WN*WAVES_N columns,
+//   64*WAVES_M*WAVES_N threads.  The C_in chunk CK depends on the tap count.
 struct TileCfg {
-  int WM, WN, WAVES_M, WAVES_N, CK;
+  int WM, WN, WAVES_M, WAVES_N;
   constexpr int MT() const { return 32 * WM * WAVES_M; }
   constexpr int NTILE() const { return 32 * WN * WAVES_N; }
   constexpr int threads() const { return 64 * WAVES_M * WAVES_N; }
@@ -48,9 +48,9 @@ struct TileCfg {
 enum TileId { TILE_M128 = 0, TILE_M64 = 1, TILE_M32 = 2, TILE_COUNT = 3 };
 
 constexpr TileCfg kTiles[TILE_COUNT] = {
-    {2, 2, 2, 2, 8},  // M128: 128 x 128 tile, 4 waves of 64x64
-    {2, 2, 1, 4, 8},  // M64 :  64 x 256 tile, 4 waves of 64x64
-    {1, 4, 1, 4, 8},  // M32 :  32 x 512 tile, 4 waves of 32x128
+    {2, 2, 2, 2},  // M128: 128 x 128 tile, 4 waves of 64x64
+    {2, 2, 1, 4},  // M64 :  64 x 256 tile, 4 waves of 64x64
+    {1, 4, 1, 4},  // M32 :  32 x 512 tile, 4 waves of 32x128
 };
 
 inline TileId tile_for_rows(int M) {
@@ -58,6 +58,25 @@ inline TileId tile_for_rows(int M) {
   if (M >= 64) return TILE_M64;
   return TILE_M32;
 }
+
+// Tap counts with a dedicated (fully unrolled) instantiation; others use the
+// runtime-KT instantiation (template KT = 0).
+constexpr bool kt_specialised(int kt) {
+  return kt == 2 || kt == 3 || kt == 5 || kt == 7 || kt == 11;
+}
+constexpr int dispatch_kt(int kt) { return kt_specialised(kt) ? kt : 0; }
+
+// Input channels per LDS chunk for an instantiation: one weight slab of
+// ~12-24 KB so that two pipeline stages leave room for 3 blocks per CU; the
+// 512-column M32 tile stages wide input rows, so its chunk is capped at 8.
+constexpr int ck_for(int dkt, int tile) {
+  return (dkt == 0 || dkt >= 7) ? 4 : (dkt >= 3 || tile == TILE_M32) ? 8 : 16;
+}
+
+// Largest (KT-1)*dilation halo an instantiation stages (sizes the per-thread
+// input-staging registers).  Checked by the host before launch.
+constexpr int kMaxDil = 16;
+constexpr int halo_max(int dkt) { return dkt == 0 ? 192 : (dkt - 1) * kMaxDil; }
 
 // Launch the conv kernel for (tile, taps, ups).  Returns a hipError_t and,
 // via *name, the kernel's template-instance name (as rocprofv3 prints it).
