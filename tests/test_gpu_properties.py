@@ -1,0 +1,187 @@
+"""GPU behaviour tests: the reference's own vocoder contract
+(tests/test_hifigan_generator.py, tests/test_hifigan_integration.py of the
+reference, restated against the MI355X module), full-size (BASELINE config 2)
+size-independent properties, and the C ABI called directly.
+
+Run on an MI355X:  python -m pytest tests -m gpu -x -q
+"""
+import ctypes
+import io
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+ATOL = 1e-4
+
+
+@pytest.fixture(scope="module")
+def dev():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    return torch.device("cuda:0")
+
+
+@pytest.fixture(scope="module")
+def v1(pkg, dev):
+    from oracle import config as C
+    sd = C.make_state_dict(C.V1, seed=0)
+    gen = pkg.HiFiGANGenerator(**C.V1.kwargs()).eval()
+    gen.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
+    return gen.to(dev), sd
+
+
+def run(gen, mel):
+    with torch.no_grad():
+        out = gen(mel)
+    torch.cuda.synchronize()
+    return out
+
+
+# ---- reference contract (tests/test_hifigan_generator.py) -------------------------
+def test_forward_shape_and_range(v1, dev):
+    gen, _ = v1
+    mel = torch.randn(2, 80, 100, device=dev)
+    wav = run(gen, mel)
+    assert wav.shape == (2, 1, 100 * 256)
+    assert wav.dtype == torch.float32
+    assert wav.min() >= -1.0 and wav.max() <= 1.0
+
+
+@pytest.mark.parametrize("T", [50, 100, 200])
+def test_different_lengths(v1, dev, T):
+    wav = run(v1[0], torch.randn(1, 80, T, device=dev))
+    assert wav.shape == (1, 1, T * 256)
+
+
+@pytest.mark.parametrize("B", [1, 4, 8])
+def test_batch_sizes(v1, dev, B):
+    wav = run(v1[0], torch.randn(B, 80, 100, device=dev))
+    assert wav.shape == (B, 1, 100 * 256)
+
+
+def test_nonexact_upsampling_shape(pkg, dev):
+    # reference test_hifigan_integration.py:147-164; oracle gives [1, 1, 10048] for T=50
+    gen = pkg.HiFiGAN(n_mels=80, upsample_rates=[5, 5, 4, 2],
+                      upsample_kernel_sizes=[10, 10, 8, 4]).to(dev).eval()
+    wav = run(gen, torch.randn(1, 80, 50, device=dev))
+    assert wav.shape == (1, 1, 10048)
+
+
+def test_generate_alias_and_logging(pkg, dev):
+    model = pkg.HiFiGAN(n_mels=80, debug_shapes=True).to(dev).eval()
+    mel = torch.randn(1, 80, 10, device=dev)
+    buf = io.StringIO()
+    old, sys.stdout = sys.stdout, buf
+    try:
+        w1 = run(model, mel)
+        w2 = model.generate(mel)
+        torch.cuda.synchronize()
+    finally:
+        sys.stdout = old
+    assert torch.equal(w1, w2)
+    out = buf.getvalue()
+    assert "[HiFiGAN]" in out and "[HiFiGANGenerator]" in out and "shape" in out.lower()
+
+
+def test_inputs_rejected(v1, dev):
+    gen, _ = v1
+    with pytest.raises(RuntimeError):
+        gen(torch.randn(1, 80, 8))  # CPU tensor: no CPU fallback
+    with pytest.raises(RuntimeError):
+        gen(torch.randn(1, 81, 8, device=dev))
+    mel = torch.randn(1, 80, 8, device=dev, requires_grad=True)
+    with pytest.raises(NotImplementedError):
+        gen(mel)
+
+
+def test_weights_follow_load_state_dict(pkg, dev):
+    from oracle import config as C, hifigan_torch as H, prng
+    cfg = C.V2STAR
+    gen = pkg.HiFiGANGenerator(**cfg.kwargs()).eval().to(dev)
+    mel = prng.mel_input(5, (1, 80, 12))
+    for seed in (1, 2):
+        sd = C.make_state_dict(cfg, seed=seed)
+        gen.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
+        wav = run(gen, torch.from_numpy(mel).to(dev)).cpu()
+        ref = H.generator_forward(H.to_torch_state(sd), cfg, torch.from_numpy(mel))
+        assert (wav - ref).abs().max().item() < ATOL
+
+
+# ---- full size (BASELINE config 2) ----------------------------------------------
+@pytest.fixture(scope="module")
+def full(v1, dev):
+    gen, sd = v1
+    g = torch.Generator().manual_seed(1234)
+    mel = torch.randn(8, 80, 1024, generator=g)
+    wav = run(gen, mel.to(dev))
+    return gen, sd, mel, wav
+
+
+def test_full_size_deterministic(full, dev):
+    gen, _, mel, wav = full
+    again = run(gen, mel.to(dev))
+    assert torch.equal(wav, again)
+
+
+def test_full_size_batch_split_invariance(full, dev):
+    gen, _, mel, wav = full
+    for b in (0, 5):
+        one = run(gen, mel[b:b + 1].to(dev))
+        assert torch.equal(one[0], wav[b])
+    pair = run(gen, mel[2:4].to(dev))
+    assert torch.equal(pair, wav[2:4])
+
+
+@pytest.mark.parametrize("item,start", [(0, 0), (3, 500), (7, 1024 - 48)])
+def test_full_size_windowed_oracle(full, item, start):
+    """Receptive field is ±13 frames; the oracle on the window
+    plus a 16-frame margin reproduces the full-size output in that window."""
+    from oracle import config as C, hifigan_torch as H
+    gen, sd, mel, wav = full
+    W, M = 48, 16
+    a, b = max(0, start - M), min(1024, start + W + M)
+    ref = H.generator_forward(H.to_torch_state(sd), C.V1, mel[item:item + 1, :, a:b])
+    ref = ref[0, 0, (start - a) * 256:(start - a + W) * 256].numpy()
+    got = wav[item, 0, start * 256:(start + W) * 256].cpu().numpy()
+    assert np.abs(got - ref).max() < ATOL
+
+
+# ---- C ABI directly ---------------------------------------------------------------
+def test_c_abi_forward_internal_workspace(pkg, full, dev):
+    gen, _, mel, wav = full
+    h = gen.hip_handle(dev)
+    lib = pkg.load_library()
+    m = mel[:2].contiguous().to(dev)
+    L = lib.hfg_out_len(h.ptr, 1024)
+    out = torch.empty(2, 1, L, device=dev)
+    assert lib.hfg_reserve(h.ptr, 2, 1024) == 0
+    rc = lib.hfg_forward(h.ptr, ctypes.c_void_p(m.data_ptr()), 2, 1024,
+                         ctypes.c_void_p(out.data_ptr()), L,
+                         ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
+    assert rc == 0, lib.hfg_last_error()
+    torch.cuda.synchronize()
+    assert torch.equal(out, wav[:2])
+    # error paths: wrong out_len, too-small workspace
+    assert lib.hfg_forward(h.ptr, ctypes.c_void_p(m.data_ptr()), 2, 1024,
+                           ctypes.c_void_p(out.data_ptr()), L + 1, None) == -22
+    assert lib.hfg_forward_ws(h.ptr, ctypes.c_void_p(m.data_ptr()), 2, 1024,
+                              ctypes.c_void_p(out.data_ptr()), L, ctypes.c_void_p(out.data_ptr()),
+                              16, None) == -22
+
+
+def test_profiling_summary(pkg, v1, dev):
+    gen, _ = v1
+    h = gen.hip_handle(dev)
+    h.profile_reset()
+    h.set_profiling(True)
+    run(gen, torch.randn(1, 80, 64, device=dev))
+    h.set_profiling(False)
+    prof = h.profile_summary()
+    assert sum(v["launches"] for v in prof.values()) == 78
+    assert all(v["ms"] > 0 for v in prof.values())
+    from oracle import config as C
+    total_flop = sum(v["flop"] for v in prof.values())
+    assert abs(total_flop - 2398848 * 64 * 256) / total_flop < 1e-5  # summary prints 7 digits
