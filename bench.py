@@ -37,6 +37,15 @@ METRIC = ("audio samples/sec/GPU (HiFi-GAN 80-mel→22.05 kHz) at 1/2/4/8 MI355X
 SAMPLE_RATE = 22050
 PEAK_FP32_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 matrix (= vector) peak
 PEAK_HBM_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+PEAK_BF16_TFLOPS = 2500.0  # MI355X_MICROARCH.md: BF16 MFMA dense (no sparsity)
+
+
+def kernel_peak(name: str):
+    """(peak in algorithmic fp32-conv TFLOP/s, description) for one kernel."""
+    if name.startswith("conv1d_bf16x3"):
+        # 3 bf16 MFMA products (hi*hi + hi*lo + lo*hi) per algorithmic multiply-add
+        return PEAK_BF16_TFLOPS / 3.0, "bf16 dense MFMA 2.5 PFLOP/s / 3 split products"
+    return PEAK_FP32_TFLOPS, "fp32 MFMA 157.3 TFLOP/s"
 
 
 def parse():
@@ -47,6 +56,10 @@ def parse():
     ap.add_argument("--preset", default="v1", choices=["v1", "v2star"])
     ap.add_argument("--batch", type=int, default=8, help="utterances per GPU")
     ap.add_argument("--frames", type=int, default=1024)
+    ap.add_argument("--precision", default="fp32", choices=["fp32", "bf16x3"],
+                    help="ResBlock conv arithmetic: exact fp32 MFMA or bf16x3 split")
+    ap.add_argument("--also", nargs="*", default=["bf16x3"],
+                    help="extra precisions measured in the same run (reported under 'alt')")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget-s", type=float, default=12.0)
     ap.add_argument("--no-profile", action="store_true",
@@ -106,10 +119,6 @@ def main():
                                         if rank == 0 else None, spec, dev, src=0)
     else:
         sd = {k: torch.from_numpy(v) for k, v in sd_np.items()}
-    gen = pkg.HiFiGANGenerator(**cfg.kwargs()).eval()
-    gen.load_state_dict({k: v.detach().cpu() for k, v in sd.items()})
-    h = gen.hip_handle(dev)
-
     # this rank's utterances of the global batch (weak scaling: batch per GPU fixed)
     global_batch = args.batch * world
     start, stop = hdist.shard_range(global_batch, world, rank)
@@ -117,41 +126,56 @@ def main():
     gmel = torch.Generator().manual_seed(1234)
     mel_all = torch.randn(global_batch, cfg.n_mels, T, generator=gmel)
     mel = mel_all[start:stop].contiguous().to(dev)
-    out_len = h.out_len(T)
-    wav = torch.empty((B, 1, out_len), dtype=torch.float32, device=dev)
-    ws_bytes = h.workspace_bytes(B, T)
-    ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
     stream = torch.cuda.current_stream(dev)
+    host_sd = {k: v.detach().cpu() for k, v in sd.items()}
 
-    def step():
-        h.forward_ws(mel.data_ptr(), B, T, wav.data_ptr(), out_len, ws.data_ptr(), ws_bytes,
-                     stream.cuda_stream)
+    def measure(precision):
+        """Warm-up, then EXACTLY args.steps timed forwards bracketed by barrier +
+        synchronize; returns (max-over-ranks seconds, per-kernel profile, out_len)."""
+        gen = pkg.HiFiGANGenerator(**cfg.kwargs(), precision=precision).eval()
+        gen.load_state_dict(host_sd)
+        h = gen.hip_handle(dev)
+        out_len = h.out_len(T)
+        wav = torch.empty((B, 1, out_len), dtype=torch.float32, device=dev)
+        ws_bytes = h.workspace_bytes(B, T)
+        ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
 
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize(dev)
+        def step():
+            h.forward_ws(mel.data_ptr(), B, T, wav.data_ptr(), out_len, ws.data_ptr(), ws_bytes,
+                         stream.cuda_stream)
 
-    profile = not args.no_profile
-    if profile:
-        h.profile_reset()
-        h.set_profiling(True)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize(dev)
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        dist.barrier()
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-    prof = {}
-    if profile:
-        h.set_profiling(False)
-        prof = h.profile_summary()
+        for _ in range(args.warmup):
+            step()
+        torch.cuda.synchronize(dev)
+        profile = not args.no_profile
+        if profile:
+            h.profile_reset()
+            h.set_profiling(True)
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            step()
+        torch.cuda.synchronize(dev)
+        elapsed = time.perf_counter() - t0
+        if world > 1:
+            dist.barrier()
+            t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            elapsed = float(t.item())
+        prof = {}
+        if profile:
+            h.set_profiling(False)
+            prof = h.profile_summary()
+        del ws, wav
+        return elapsed, prof, out_len
+
+    elapsed, prof, out_len = measure(args.precision)
+    alt = {}
+    for prec in args.also:
+        if prec != args.precision:
+            alt[prec] = measure(prec)
 
     samples_total = global_batch * out_len * args.steps
     value = samples_total / elapsed
@@ -173,7 +197,7 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "f32",
+        "dtype": "f32" if args.precision == "fp32" else "f32 in/out, bf16x3 split products",
         "data": "synthetic: mel ~ N(0,1) (torch seed 1234), PRNG default-init V1 weights "
                 "(no checkpoint)",
         "config": {
@@ -187,6 +211,30 @@ def main():
         "per_gpu": value / world,
         "rtf": (elapsed / args.steps) / (args.batch * out_len / SAMPLE_RATE),
     }
+    def roofline(prof, ms_per_step):
+        dom_name, dom = max(prof.items(), key=lambda kv: kv[1]["ms"])
+        achieved = dom["flop"] / (dom["ms"] * 1e-3) / 1e12
+        peak, peak_note = kernel_peak(dom_name)
+        return {"bound": "mfma", "kernel": dom_name, "achieved": achieved, "peak": peak,
+                "peak_note": peak_note, "unit": "TFLOP/s", "frac": achieved / peak,
+                "avg_launch_ms": dom["ms"] / dom["launches"],
+                "flop_per_launch": dom["flop"] / dom["launches"],
+                "share_of_step": dom["ms"] / args.steps / ms_per_step}
+
+    if alt:
+        line["alt"] = {}
+        for prec, (el, pr, ol) in alt.items():
+            v = global_batch * ol * args.steps / el
+            entry = {"value": v, "ms_per_step": 1000.0 * el / args.steps,
+                     "rtf": (el / args.steps) / (args.batch * ol / SAMPLE_RATE),
+                     "speedup_vs_headline": v / value,
+                     "parity": "atol 1e-4 vs reference fixtures (tests/test_gpu_parity.py)"}
+            if pr:
+                entry["roofline"] = roofline(pr, 1000.0 * el / args.steps)
+                entry["kernels"] = {k: {"launches": q["launches"] // args.steps,
+                                        "ms_per_step": q["ms"] / args.steps}
+                                    for k, q in sorted(pr.items(), key=lambda kv: -kv[1]["ms"])}
+            line["alt"][prec] = entry
     if prof:
         tot_ms = sum(v["ms"] for v in prof.values()) / args.steps
         dom_name, dom = max(prof.items(), key=lambda kv: kv[1]["ms"])
@@ -200,13 +248,15 @@ def main():
                     traffic = pmc[dom_name]["bytes_per_launch"]
             except Exception:
                 traffic = None
+        peak, peak_note = kernel_peak(dom_name)
         line["roofline"] = {
             "bound": "mfma",
             "kernel": dom_name,
             "achieved": achieved,
-            "peak": PEAK_FP32_TFLOPS,
+            "peak": peak,
+            "peak_note": peak_note,
             "unit": "TFLOP/s",
-            "frac": achieved / PEAK_FP32_TFLOPS,
+            "frac": achieved / peak,
             "traffic": traffic,
             "launches_per_step": dom["launches"] / args.steps,
             "avg_launch_ms": dom["ms"] / dom["launches"],

@@ -52,6 +52,17 @@ extern "C" {
 #define HFG_EAGAIN (-11)   /* weights incomplete (a key was never set)    */
 #define HFG_EIO (-5)       /* HIP runtime error (launch, memcpy, ...)     */
 
+/* Arithmetic of the ResBlock / conv_pre convolutions (the upsamplers, the
+ * C<64 stages and conv_post always run the exact fp32 kernels).
+ *   FP32   : fp32 operands on the fp32 matrix cores (v_mfma_f32_32x32x2_f32),
+ *            exact fp32 products (the parity reference mode).
+ *   BF16X3 : every fp32 operand split as hi = bf16(v), lo = bf16(v - hi);
+ *            hi*hi + hi*lo + lo*hi accumulated in fp32 on the bf16 matrix cores
+ *            (~16-bit-mantissa products, 5.3x the fp32 MFMA rate).  Output
+ *            within ~1e-6 of the reference, inside the 1e-4 parity bar. */
+#define HFG_DTYPE_FP32 0
+#define HFG_DTYPE_BF16X3 1
+
 typedef struct hfg_handle hfg_handle;
 
 /* Hyper-parameters: models/hifigan.py:149-158 constructor arguments. */
@@ -65,7 +76,7 @@ typedef struct hfg_config {
     int32_t res_kernels[HFG_MAX_RES];            /* [3, 7, 11]                */
     int32_t n_dil[HFG_MAX_RES];                  /* len(dilations[j])         */
     int32_t dil[HFG_MAX_RES][HFG_MAX_DIL];       /* [[1,3,5],[1,3,5],[1,3,5]] */
-    int32_t dtype;                               /* 0 = fp32 (only value)     */
+    int32_t dtype;                               /* HFG_DTYPE_*               */
 } hfg_config;
 
 /* Library version string, e.g. "hifigan_hip 0.1.0 gfx950". */

@@ -38,15 +38,15 @@ def test_library_exports_every_header_symbol(pkg):
     assert b"gfx950" in lib.hfg_version()
 
 
-def host_handle(pkg, cfg):
-    c = pkg.make_config(**{k: v for k, v in cfg.kwargs().items()})
+def host_handle(pkg, cfg, precision="fp32"):
+    c = pkg.make_config(**{k: v for k, v in cfg.kwargs().items()}, precision=precision)
     return pkg.Handle(c, -1)
 
 
 def test_create_validates_config(pkg):
     lib = pkg.load_library()
     c = pkg.make_config(80, [8, 8, 2, 2], [16, 16, 4, 4], 512, [3, 7, 11], [[1, 3, 5]] * 3)
-    c.dtype = 1
+    c.dtype = 7
     h = ctypes.c_void_p()
     assert lib.hfg_create(ctypes.byref(c), -1, ctypes.byref(h)) == -22
     assert b"dtype" in lib.hfg_last_error()
@@ -200,3 +200,57 @@ def test_weight_norm_fold(pkg):
         _, b, bb = h2.packed_layer(mod)
         assert np.allclose(a, b, rtol=1e-6, atol=1e-7)
         assert np.array_equal(ab, bb)
+
+
+def bf2f(u16):
+    return (u16.astype(np.uint32) << 16).view(np.float32)
+
+
+@pytest.mark.parametrize("preset", ["v1", "v2star"])
+def test_bf16x3_packing(pkg, preset):
+    """bf16x3 layers: the packed hi/lo planes reconstruct every weight to ~2^-16
+    relative, in the fragment order of conv_bf16x3.hip."""
+    cfg = C.PRESETS[preset]
+    sd = C.make_state_dict(cfg, seed=31)
+    h = host_handle(pkg, cfg, "bf16x3")
+    for k, v in sd.items():
+        h.set_weight(k, torch.from_numpy(v))
+    h.commit()
+    WAVES = {0: (2, 2), 1: (1, 2)}  # tile -> (WAVES_M, WM) of kBf16x3Tiles
+    TPC = 4
+    n_checked = 0
+    for mod in ["conv_pre", "mrfs.0.resblocks.2.convs1.1", "mrfs.1.resblocks.0.convs2.1",
+                "mrfs.2.resblocks.1.convs1.0", "mrfs.3.resblocks.2.convs2.1"]:
+        info, packed, bias = h.packed_layer(mod)
+        W = sd[mod + ".weight"]
+        cout, cin, k = W.shape
+        if info["CK"] != 16:  # fp32 layer (C < 64 stage)
+            assert cout < 64
+            continue
+        n_checked += 1
+        wm_, WM = WAVES[info["tile"]]
+        MT = info["MT"]
+        n_g, n_tg = -(-cin // 16), -(-k // TPC)
+        assert info["n_chunks"] == n_g * n_tg
+        u = packed.view(np.uint16).reshape(info["m_tiles"], n_g, n_tg, TPC, 2, wm_, WM, 64, 8)
+        hi = bf2f(u[:, :, :, :, 0])
+        lo = bf2f(u[:, :, :, :, 1])
+        rec = np.zeros((info["m_tiles"] * MT, n_g * 16, n_tg * TPC), np.float64)
+        lane = np.arange(64)
+        for mt in range(info["m_tiles"]):
+            for g in range(n_g):
+                for tg in range(n_tg):
+                    for jj in range(TPC):
+                        for wv in range(wm_):
+                            for wm in range(WM):
+                                rows = mt * MT + wv * 32 * WM + wm * 32 + (lane & 31)
+                                for e in range(8):
+                                    cis = g * 16 + 8 * (lane >> 5) + e
+                                    val = (hi[mt, g, tg, jj, wv, wm, :, e].astype(np.float64)
+                                           + lo[mt, g, tg, jj, wv, wm, :, e])
+                                    rec[rows, cis, tg * TPC + jj] = val
+        rec = rec[:cout, :cin, :k]
+        err = np.abs(rec - W).max() / np.abs(W).max()
+        assert err < 2.0 ** -15, (mod, err)
+        assert np.array_equal(bias[:cout], sd[mod + ".bias"])
+    assert n_checked >= 2

@@ -20,8 +20,8 @@ def _dev():
     return torch.device("cuda:0")
 
 
-def _gen(pkg, cfg, sd, dev):
-    gen = pkg.HiFiGANGenerator(**cfg.kwargs()).eval()
+def _gen(pkg, cfg, sd, dev, precision="fp32"):
+    gen = pkg.HiFiGANGenerator(**cfg.kwargs(), precision=precision).eval()
     if any(k.endswith("weight_g") for k in sd):
         gen.apply_weight_norm()
     gen.load_state_dict({k: torch.from_numpy(np.ascontiguousarray(v)) for k, v in sd.items()})
@@ -75,4 +75,35 @@ def test_random_vs_oracle(pkg, preset, B, T):
     assert wav.shape == ref.shape
     err = np.abs(wav - ref).max()
     print(f"{preset} B={B} T={T}: max err {err:.3e}")
+    assert err < ATOL
+
+
+@pytest.mark.parametrize("name", GOLDEN)
+def test_golden_fixture_bf16x3(pkg, golden_index, name):
+    """Split-precision mode (bf16 hi/lo operands, fp32 accumulate) meets the same
+    1e-4 bar against the reference outputs."""
+    dev = _dev()
+    case = golden_index["cases"][name]
+    cfg, sd = golden_case_state(case)
+    g = load_golden(name)
+    gen = _gen(pkg, cfg, sd, dev, precision="bf16x3")
+    wav = _run(gen, g["mel"], dev)
+    err = np.abs(wav - g["wav"]).max()
+    print(f"{name} [bf16x3]: max|hip-ref| = {err:.3e}")
+    assert err < ATOL
+    rel = np.linalg.norm(wav - g["wav"]) / np.linalg.norm(g["wav"])
+    assert rel < 1e-3, rel
+
+
+@pytest.mark.parametrize("preset,B,T", [("v1", 2, 300), ("v2star", 2, 200)])
+def test_bf16x3_vs_oracle_longer(pkg, preset, B, T):
+    from oracle import config as C, prng
+    dev = _dev()
+    cfg = C.PRESETS[preset]
+    sd = C.make_state_dict(cfg, seed=7)
+    mel = prng.mel_input(70 + T, (B, cfg.n_mels, T))
+    wav = _run(_gen(pkg, cfg, sd, dev, precision="bf16x3"), mel, dev)
+    ref = _oracle(cfg, sd, mel)
+    err = np.abs(wav - ref).max()
+    print(f"{preset} B={B} T={T} [bf16x3]: max err {err:.3e}")
     assert err < ATOL

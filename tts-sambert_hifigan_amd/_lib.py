@@ -53,8 +53,11 @@ class HfgConfig(ctypes.Structure):
     ]
 
 
+DTYPES = {"fp32": 0, "bf16x3": 1}
+
+
 def make_config(n_mels, upsample_rates, upsample_kernel_sizes, upsample_initial_channel,
-                resblock_kernel_sizes, resblock_dilation_sizes) -> HfgConfig:
+                resblock_kernel_sizes, resblock_dilation_sizes, precision: str = "fp32") -> HfgConfig:
     if len(upsample_rates) != len(upsample_kernel_sizes):
         raise ValueError("upsample_rates and upsample_kernel_sizes differ in length")
     if len(resblock_kernel_sizes) != len(resblock_dilation_sizes):
@@ -79,7 +82,9 @@ def make_config(n_mels, upsample_rates, upsample_kernel_sizes, upsample_initial_
         c.n_dil[j] = len(dils)
         for m, d in enumerate(dils):
             c.dil[j][m] = int(d)
-    c.dtype = 0
+    if precision not in DTYPES:
+        raise ValueError(f"precision must be one of {sorted(DTYPES)}")
+    c.dtype = DTYPES[precision]
     return c
 
 

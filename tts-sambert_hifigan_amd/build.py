@@ -12,7 +12,7 @@ PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(PKG_DIR, "csrc")
 LIB_NAME = "libhifigan_hip.so"
 LIB_PATH = os.path.join(PKG_DIR, LIB_NAME)
-SOURCES = ["conv_kernels.hip", "hifigan_capi.cpp"]
+SOURCES = ["conv_kernels.hip", "conv_bf16x3.hip", "hifigan_capi.cpp"]
 HEADERS = ["kernels.h", os.path.join("..", "..", "include", "hifigan_hip.h"),
            os.path.join("..", "..", "include", "hifigan_hip_inspect.h")]
 

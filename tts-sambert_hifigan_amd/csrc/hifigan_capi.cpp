@@ -53,6 +53,7 @@ struct Layer {
   int s, p;          // ConvTranspose1d stride / padding
   // GEMM view
   int M, KT, CK, tile, m_tiles, n_chunks;
+  int prec;          // 0: fp32 MFMA kernel, 1: bf16x3 split-precision kernel
   size_t w_off, b_off;  // offsets (floats) into the packed device buffer
   size_t w_len, b_len;
 };
@@ -118,7 +119,8 @@ int validate_config(const hfg_config* c) {
   if (c->n_mels <= 0) return fail(HFG_EINVAL, "n_mels must be > 0");
   if (c->n_up <= 0 || c->n_up > HFG_MAX_STAGES) return fail(HFG_EINVAL, "n_up out of range");
   if (c->n_res <= 0 || c->n_res > HFG_MAX_RES) return fail(HFG_EINVAL, "n_res out of range");
-  if (c->dtype != 0) return fail(HFG_EINVAL, "only dtype 0 (fp32) is supported");
+  if (c->dtype != HFG_DTYPE_FP32 && c->dtype != HFG_DTYPE_BF16X3)
+    return fail(HFG_EINVAL, "dtype must be HFG_DTYPE_FP32 (0) or HFG_DTYPE_BF16X3 (1)");
   if (c->c0 <= 0) return fail(HFG_EINVAL, "upsample_initial_channel must be > 0");
   for (int i = 0; i < c->n_up; ++i) {
     if (c->up_rates[i] <= 0 || c->up_kernels[i] <= 0)
@@ -215,6 +217,25 @@ void build_layers(hfg_handle* h) {
       off += 64;
       continue;
     }
+    if (h->cfg.dtype == HFG_DTYPE_BF16X3 && L.kind == L_CONV &&
+        hfg::bf16x3_tile_for_rows(L.M) >= 0) {
+      // split-precision path: chunk = 16 channels x kBf16x3Tpc taps
+      const hfg::Bf16x3Cfg& t3 = hfg::kBf16x3Tiles[hfg::bf16x3_tile_for_rows(L.M)];
+      L.prec = 1;
+      L.tile = hfg::bf16x3_tile_for_rows(L.M);
+      L.CK = hfg::kBf16x3Ck;
+      L.m_tiles = (L.M + t3.MT() - 1) / t3.MT();
+      L.n_chunks = ((L.C_in + L.CK - 1) / L.CK) * ((L.KT + hfg::kBf16x3Tpc - 1) / hfg::kBf16x3Tpc);
+      const size_t slab_bf16 = (size_t)hfg::kBf16x3Tpc * 2 * t3.MT() * 16;
+      L.w_off = off;
+      L.w_len = (size_t)L.m_tiles * L.n_chunks * slab_bf16 / 2;  // in floats
+      off += (L.w_len + 63) & ~(size_t)63;
+      L.b_off = off;
+      L.b_len = (size_t)L.m_tiles * t3.MT();
+      off += (L.b_len + 63) & ~(size_t)63;
+      continue;
+    }
+    L.prec = 0;
     L.tile = hfg::tile_for_rows(L.M);
     const TileCfg& t = kTiles[L.tile];
     L.CK = hfg::ck_for(hfg::dispatch_kt(L.KT), L.tile);
@@ -252,6 +273,51 @@ void pack_gemm_weights(const Layer& L, F wt, float* dst) {
               }
 }
 
+// float -> bf16, round to nearest even (NaN stays NaN)
+inline uint16_t f2bf(float f) {
+  uint32_t u;
+  memcpy(&u, &f, 4);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return (uint16_t)((u >> 16) | 0x40u);
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return (uint16_t)(u >> 16);
+}
+inline float bf2f(uint16_t b) {
+  uint32_t u = (uint32_t)b << 16;
+  float f;
+  memcpy(&f, &u, 4);
+  return f;
+}
+
+// A-fragment order of conv1d_bf16x3 (conv_bf16x3.hip), in bf16 elements:
+//   idx = ((((((mt*n_g + g)*n_tg + tg)*TPC + jj)*2 + plane)*WAVES_M + wave_m)*WM + wm)*512
+//         + lane*8 + e
+//   row = mt*MT + wave_m*32*WM + wm*32 + (lane & 31), ci = g*16 + 8*(lane >> 5) + e,
+//   tap = tg*TPC + jj; plane 0 = bf16(w), plane 1 = bf16(w - hi).
+void pack_bf16x3(const Layer& L, const float* w, uint16_t* dst) {
+  const hfg::Bf16x3Cfg& t = hfg::kBf16x3Tiles[L.tile];
+  const int TPC = hfg::kBf16x3Tpc;
+  const int n_g = (L.C_in + 15) / 16, n_tg = (L.KT + TPC - 1) / TPC;
+  size_t idx = 0;
+  for (int mt = 0; mt < L.m_tiles; ++mt)
+    for (int g = 0; g < n_g; ++g)
+      for (int tg = 0; tg < n_tg; ++tg)
+        for (int jj = 0; jj < TPC; ++jj)
+          for (int plane = 0; plane < 2; ++plane)
+            for (int wave_m = 0; wave_m < t.WAVES_M; ++wave_m)
+              for (int wm = 0; wm < t.WM; ++wm)
+                for (int lane = 0; lane < 64; ++lane)
+                  for (int e = 0; e < 8; ++e) {
+                    const int row = mt * t.MT() + wave_m * 32 * t.WM + wm * 32 + (lane & 31);
+                    const int ci = g * 16 + 8 * (lane >> 5) + e;
+                    const int tap = tg * TPC + jj;
+                    float v = 0.f;
+                    if (row < L.M && ci < L.C_in && tap < L.KT)
+                      v = w[((size_t)row * L.C_in + ci) * L.k + tap];
+                    const uint16_t hi = f2bf(v);
+                    dst[idx++] = plane == 0 ? hi : f2bf(v - bf2f(hi));
+                  }
+}
+
 void pack_layer(hfg_handle* h, const Layer& L) {
   const Param& W = h->params[L.mod + ".weight"];
   const Param& Bp = h->params[L.mod + ".bias"];
@@ -261,6 +327,11 @@ void pack_layer(hfg_handle* h, const Layer& L) {
   if (L.kind == L_POST) {
     std::memcpy(dst, w, sizeof(float) * L.C_in * 7);  // [1][C][7]
     bdst[0] = Bp.data[0];
+    return;
+  }
+  if (L.kind == L_CONV && L.prec == 1) {
+    pack_bf16x3(L, w, reinterpret_cast<uint16_t*>(dst));
+    for (size_t m = 0; m < L.b_len; ++m) bdst[m] = m < (size_t)L.M ? Bp.data[m] : 0.f;
     return;
   }
   if (L.kind == L_CONV) {
@@ -381,7 +452,6 @@ struct Launcher {
 int run_conv(hfg_handle* h, Launcher& ln, const Layer& L, const float* x, int64_t B, int64_t Lt,
              float* y, bool act_in, bool act_out, const float* res, float* mrf, int mrf_mode,
              float mrf_div) {
-  const TileCfg& t = kTiles[L.tile];
   ConvParams p{};
   p.x = x;
   p.x_bs = (int64_t)L.C_in * Lt;
@@ -403,15 +473,19 @@ int run_conv(hfg_handle* h, Launcher& ln, const Layer& L, const float* x, int64_
   p.mrf_mode = mrf_mode;
   p.mrf_div = mrf_div;
   p.n_chunks = L.n_chunks;
-  const int n_tiles = (int)((Lt + t.NTILE() - 1) / t.NTILE());
+  const int ntile = L.prec == 1 ? hfg::kBf16x3Tiles[L.tile].NTILE() : kTiles[L.tile].NTILE();
+  const int n_tiles = (int)((Lt + ntile - 1) / ntile);
   const double flop = 2.0 * L.C_out * L.C_in * L.k * (double)Lt * B;
   double bytes = 4.0 * B * Lt * (L.C_in + L.C_out) + 4.0 * L.C_out * L.C_in * L.k;
   if (res) bytes += 4.0 * B * Lt * L.C_out;
   if (mrf && (mrf_mode & 1)) bytes += 4.0 * B * Lt * L.C_out;
   const char* name = nullptr;
   ln.begin(flop, bytes);
-  hipError_t e = hfg::launch_conv((TileId)L.tile, L.KT, false, p, n_tiles, L.m_tiles, (int)B,
-                                  ln.stream, &name);
+  hipError_t e = L.prec == 1
+                     ? hfg::launch_conv_bf16x3(L.tile, L.KT, p, n_tiles, L.m_tiles, (int)B,
+                                               ln.stream, &name)
+                     : hfg::launch_conv((TileId)L.tile, L.KT, false, p, n_tiles, L.m_tiles,
+                                        (int)B, ln.stream, &name);
   ln.end(name);
   if (e != hipSuccess) return fail(HFG_EIO, "launch %s: %s", L.mod.c_str(), hipGetErrorString(e));
   return HFG_OK;
@@ -533,7 +607,7 @@ int forward_impl(hfg_handle* h, const float* mel, int64_t B, int64_t T, float* w
 // ============================================================================
 extern "C" {
 
-const char* hfg_version(void) { return "hifigan_hip 0.1.0 gfx950 fp32-mfma"; }
+const char* hfg_version(void) { return "hifigan_hip 0.2.0 gfx950 fp32-mfma bf16x3-mfma"; }
 
 const char* hfg_last_error(void) { return g_err.c_str(); }
 
@@ -775,7 +849,9 @@ int hfg_debug_packed_layer(hfg_handle* h, const char* mod, float* out, size_t ca
       info[6] = (int64_t)L.w_len;
       info[7] = (int64_t)L.b_len;
       info[8] = L.CK;
-      info[9] = L.kind == L_POST ? 0 : kTiles[L.tile].MT();
+      info[9] = L.kind == L_POST ? 0
+                : L.prec == 1    ? hfg::kBf16x3Tiles[L.tile].MT()
+                                 : kTiles[L.tile].MT();
     }
     if (!out) return HFG_OK;
     if (h->dirty) {

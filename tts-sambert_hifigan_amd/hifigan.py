@@ -87,6 +87,8 @@ class HiFiGANGenerator(nn.Module):
         resblock_kernel_sizes: List[int] = [3, 7, 11],
         resblock_dilation_sizes: List[List[int]] = [[1, 3, 5], [1, 3, 5], [1, 3, 5]],
         debug_shapes: bool = False,
+        *,
+        precision: str = "fp32",
     ):
         super().__init__()
         self.n_mels = n_mels
@@ -107,11 +109,20 @@ class HiFiGANGenerator(nn.Module):
         final_channels = upsample_initial_channel // (2 ** self.num_upsamples)
         self.conv_post = nn.Conv1d(final_channels, 1, kernel_size=7, stride=1, padding=3)
 
-        self._hfg_cfg = _lib.make_config(n_mels, upsample_rates, upsample_kernel_sizes,
-                                         upsample_initial_channel, resblock_kernel_sizes,
-                                         resblock_dilation_sizes)
+        self._hfg_args = (n_mels, upsample_rates, upsample_kernel_sizes, upsample_initial_channel,
+                          resblock_kernel_sizes, resblock_dilation_sizes)
         self._hfg_handles: Dict[int, _lib.Handle] = {}
         self._hfg_fingerprint: Dict[int, tuple] = {}
+        self.set_precision(precision)
+
+    def set_precision(self, precision: str):
+        """"fp32" (exact fp32 MFMA, default) or "bf16x3" (fp32 operands split into
+        two bf16 halves on the bf16 matrix cores; within ~1e-6 of the reference)."""
+        self._hfg_cfg = _lib.make_config(*self._hfg_args, precision=precision)
+        self.precision = precision
+        self._hfg_handles = {}
+        self._hfg_fingerprint = {}
+        return self
 
     # ------------------------------------------------------------------
     def _weight_tensors(self):
@@ -238,7 +249,8 @@ class HiFiGAN(nn.Module):
                  resblock_kernel_sizes: List[int] = [3, 7, 11],
                  resblock_dilation_sizes: List[List[int]] = [[1, 3, 5], [1, 3, 5], [1, 3, 5]],
                  msd_use_spectral_norm: bool = False, mpd_periods: List[int] = [2, 3, 5, 7, 11],
-                 mpd_use_spectral_norm: bool = False, debug_shapes: bool = False):
+                 mpd_use_spectral_norm: bool = False, debug_shapes: bool = False, *,
+                 precision: str = "fp32"):
         super().__init__()
         self.debug_shapes = debug_shapes or os.getenv("DEBUG_SHAPES", "0") == "1"
         self.generator = HiFiGANGenerator(
@@ -246,7 +258,8 @@ class HiFiGAN(nn.Module):
             upsample_kernel_sizes=upsample_kernel_sizes,
             upsample_initial_channel=upsample_initial_channel,
             resblock_kernel_sizes=resblock_kernel_sizes,
-            resblock_dilation_sizes=resblock_dilation_sizes, debug_shapes=debug_shapes)
+            resblock_dilation_sizes=resblock_dilation_sizes, debug_shapes=debug_shapes,
+            precision=precision)
         self.msd = None
         self.mpd = None
 
