@@ -15,6 +15,9 @@
  *   hfg_forward[_ws]    ← HiFiGANGenerator.forward         models/hifigan.py:224-261
  *   hfg_out_len         ← output-length contract           models/hifigan.py:195-203
  *                         ((L-1)u - 2((k-u)//2) + k per stage)
+ *   hfg_forward_ex      ← acoustic→vocoder glue (spec-only in the reference,
+ *                         .kiro/specs/.../design.md:905-906): [B,T,80] input
+ *                         and per-utterance lengths of a padded batch
  *
  * Conventions
  *   - Every int-returning call returns 0 on success or a negative errno-style
@@ -124,6 +127,27 @@ int hfg_forward(hfg_handle* h, const float* mel, int64_t B, int64_t T,
 int hfg_forward_ws(hfg_handle* h, const float* mel, int64_t B, int64_t T,
                    float* wav, int64_t out_len, void* workspace,
                    size_t workspace_bytes, void* stream);
+
+/* Acoustic-model glue (design.md:905-906 of the
+ * reference spec: mel_pred.transpose(1,2) -> HiFiGAN(mel)).
+ *   mel_layout HFG_MEL_BTC reads mel as [B][T][n_mels] — the layout
+ *   SAMBERTAcousticModel.inference emits (models/acoustic_model.py:267-297) —
+ *   with the transpose fused into conv_pre's input staging.
+ *   lengths (device int32[B], or NULL): valid frames per utterance of a
+ *   zero-padded batch.  Every layer zero-pads at the utterance's own length,
+ *   so wav[b][0][0 : hfg_out_len(len_b)] equals the Generator run on
+ *   mel[b, :, :len_b] alone; samples past it are 0.  Tiles past an
+ *   utterance's end are skipped. */
+#define HFG_MEL_BCT 0
+#define HFG_MEL_BTC 1
+typedef struct hfg_forward_opts {
+    int32_t mel_layout;      /* HFG_MEL_BCT (default) or HFG_MEL_BTC          */
+    const int32_t* lengths;  /* device int32[B] valid frames, or NULL (all T)  */
+} hfg_forward_opts;
+
+int hfg_forward_ex(hfg_handle* h, const float* mel, int64_t B, int64_t T,
+                   const hfg_forward_opts* opts, float* wav, int64_t out_len,
+                   void* workspace, size_t workspace_bytes, void* stream);
 
 /* Per-launch profiling with HIP events recorded on the launch stream.
  * While enabled, every kernel launch of hfg_forward* is bracketed by an

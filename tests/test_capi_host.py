@@ -31,7 +31,7 @@ def header_symbols():
 def test_library_exports_every_header_symbol(pkg):
     lib = pkg.load_library()
     syms = header_symbols()
-    assert len(syms) == 16
+    assert len(syms) == 17
     for s in sorted(syms):
         assert hasattr(lib, s), f"missing export {s}"
     assert set(syms) == set(pkg._lib.SIGNATURES), "ctypes signatures out of sync with headers"
@@ -63,7 +63,7 @@ def test_out_len_and_workspace(pkg):
             assert h.out_len(t) == C.out_len(cfg, t)
         assert h.workspace_bytes(8, 1024) >= 4 * 4 * 8 * 128 * 65536 * (cfg is C.V1)
     h = host_handle(pkg, C.V1)
-    assert h.workspace_bytes(8, 1024) == 4 * 4 * 8 * 128 * 65536
+    assert 0 <= h.workspace_bytes(8, 1024) - 4 * 4 * 8 * 128 * 65536 <= 4096
     assert pkg.load_library().hfg_num_params(h.ptr) == 156
 
 

@@ -1,0 +1,94 @@
+"""SURVEY.md §8(f) rows 2-3 on the GPU: acoustic-model glue ([B, T, 80] input,
+ragged batches) and streaming vocoding, both against the one-shot Generator
+(bitwise) and the CPU oracle (atol 1e-4)."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+ATOL = 1e-4
+
+
+@pytest.fixture(scope="module")
+def dev():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    return torch.device("cuda:0")
+
+
+@pytest.fixture(scope="module", params=["fp32", "bf16x3"])
+def gen_sd(pkg, dev, request):
+    from oracle import config as C
+    sd = C.make_state_dict(C.V1, seed=4)
+    gen = pkg.HiFiGANGenerator(**C.V1.kwargs(), precision=request.param).eval()
+    gen.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
+    return gen.to(dev), sd
+
+
+def run(gen, mel, **kw):
+    with torch.no_grad():
+        out = gen(mel, **kw)
+    torch.cuda.synchronize()
+    return out
+
+
+def test_btc_layout_equals_bct(gen_sd, dev):
+    gen, _ = gen_sd
+    mel = torch.randn(3, 80, 57, device=dev)
+    a = run(gen, mel)
+    b = run(gen, mel.transpose(1, 2).contiguous(), mel_layout="btc")
+    assert torch.equal(a, b)
+
+
+def test_ragged_batch_equals_per_utterance(pkg, gen_sd, dev):
+    import importlib
+    glue = importlib.import_module("tts_sambert_hifigan_amd.glue")
+    from oracle import config as C, hifigan_torch as H
+    gen, sd = gen_sd
+    lens = [61, 40, 7, 1]
+    T = max(lens)
+    g = torch.Generator().manual_seed(3)
+    mel_pred = torch.randn(len(lens), T, 80, generator=g)  # acoustic-model layout
+    for b, n in enumerate(lens):
+        mel_pred[b, n:] = 123.0  # garbage in the padding must not leak
+    wavs = glue.vocode_acoustic(gen, mel_pred.to(dev), lens)
+    full = run(gen, mel_pred.to(dev), lengths=lens, mel_layout="btc")
+    for b, n in enumerate(lens):
+        alone = run(gen, mel_pred[b:b + 1, :n].transpose(1, 2).contiguous().to(dev))
+        assert wavs[b].shape[0] == n * 256
+        assert torch.equal(wavs[b], alone[0, 0]), b
+        assert torch.count_nonzero(full[b, 0, n * 256:]) == 0
+        ref = H.generator_forward(H.to_torch_state(sd), C.V1, mel_pred[b:b + 1, :n].transpose(1, 2))
+        assert (wavs[b].cpu() - ref[0, 0]).abs().max().item() < ATOL
+
+
+def test_vocode_list(pkg, gen_sd, dev):
+    import importlib
+    glue = importlib.import_module("tts_sambert_hifigan_amd.glue")
+    gen, _ = gen_sd
+    mels = [torch.randn(80, n, device=dev) for n in (33, 5, 48)]
+    wavs = glue.vocode_list(gen, mels)
+    for m, w in zip(mels, wavs):
+        assert torch.equal(w, run(gen, m[None])[0, 0])
+
+
+def test_streaming_equals_one_shot(pkg, gen_sd, dev):
+    import importlib
+    glue = importlib.import_module("tts_sambert_hifigan_amd.glue")
+    gen, _ = gen_sd
+    assert gen.receptive_field_frames() == 15
+    T = 230
+    mel = torch.randn(80, T, device=dev)
+    ref = run(gen, mel[None])[0, 0]
+    sv = glue.StreamingVocoder(gen, chunk_frames=40)
+    pieces, pos = [], 0
+    rng = np.random.default_rng(0)
+    while pos < T:
+        n = int(rng.integers(1, 37))
+        pieces.append(sv.push(mel[:, pos:pos + n]))
+        pos += n
+    pieces.append(sv.flush())
+    out = torch.cat(pieces)
+    torch.cuda.synchronize()
+    assert out.shape == ref.shape
+    assert torch.equal(out, ref)

@@ -38,6 +38,13 @@ class HfgError(RuntimeError):
         self.code = code
 
 
+class HfgForwardOpts(ctypes.Structure):
+    _fields_ = [("mel_layout", c_int32), ("lengths", c_void_p)]
+
+
+MEL_LAYOUTS = {"bct": 0, "btc": 1}
+
+
 class HfgConfig(ctypes.Structure):
     _fields_ = [
         ("n_mels", c_int32),
@@ -105,6 +112,8 @@ SIGNATURES = {
     "hfg_forward": (c_int, [c_void_p, c_void_p, c_int64, c_int64, c_void_p, c_int64, c_void_p]),
     "hfg_forward_ws": (c_int, [c_void_p, c_void_p, c_int64, c_int64, c_void_p, c_int64,
                                c_void_p, c_size_t, c_void_p]),
+    "hfg_forward_ex": (c_int, [c_void_p, c_void_p, c_int64, c_int64, POINTER(HfgForwardOpts),
+                               c_void_p, c_int64, c_void_p, c_size_t, c_void_p]),
     "hfg_set_profiling": (c_int, [c_void_p, c_int]),
     "hfg_profile_reset": (c_int, [c_void_p]),
     "hfg_profile_summary": (c_int, [c_void_p, c_char_p, c_size_t]),
@@ -176,6 +185,13 @@ class Handle:
     def forward_ws(self, mel_ptr: int, B: int, T: int, wav_ptr: int, out_len: int, ws_ptr: int,
                    ws_bytes: int, stream: int):
         check(self.lib.hfg_forward_ws(self.ptr, c_void_p(mel_ptr), int(B), int(T),
+                                      c_void_p(wav_ptr), int(out_len), c_void_p(ws_ptr),
+                                      int(ws_bytes), c_void_p(stream)))
+
+    def forward_ex(self, mel_ptr: int, B: int, T: int, wav_ptr: int, out_len: int, ws_ptr: int,
+                   ws_bytes: int, stream: int, mel_layout: str = "bct", lengths_ptr: int = 0):
+        o = HfgForwardOpts(MEL_LAYOUTS[mel_layout], c_void_p(lengths_ptr) if lengths_ptr else None)
+        check(self.lib.hfg_forward_ex(self.ptr, c_void_p(mel_ptr), int(B), int(T), ctypes.byref(o),
                                       c_void_p(wav_ptr), int(out_len), c_void_p(ws_ptr),
                                       int(ws_bytes), c_void_p(stream)))
 

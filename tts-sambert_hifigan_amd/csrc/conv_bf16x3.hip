@@ -66,6 +66,9 @@ conv1d_bf16x3(const ConvParams p) {
   const float* __restrict__ xb = p.x + (int64_t)b * p.x_bs;
   const __bf16* __restrict__ wsrc =
       reinterpret_cast<const __bf16*>(p.w) + (int64_t)mt * p.n_chunks * SLAB;
+  const int L_in_b = p.len_in ? p.len_in[b] : p.L_in;
+  const int N_b = p.len_out ? p.len_out[b] : p.N;
+  if (n0 >= N_b) return;  // whole tile past this utterance's end (block-uniform)
 
   auto taps_in = [&](int c) {
     const int tg = c % n_tg;
@@ -94,11 +97,11 @@ conv1d_bf16x3(const ConvParams p) {
       const int t = i >> 1;
       const int cb = g * 16 + (i & 1) * 8;
       const int gi = ws + t;
-      const bool tok = (i < 2 * XW) && ((unsigned)gi < (unsigned)p.L_in);
+      const bool tok = (i < 2 * XW) && ((unsigned)gi < (unsigned)L_in_b);
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         const bool ok = tok && (cb + e < p.C_in);
-        const int64_t idx = ok ? (int64_t)(cb + e) * p.L_in + gi : 0;
+        const int64_t idx = ok ? (int64_t)(cb + e) * p.x_cs + (int64_t)gi * p.x_ts : 0;
         const float v = xb[idx];
         xv[q][e] = ok ? v : 0.f;
       }
@@ -203,7 +206,7 @@ conv1d_bf16x3(const ConvParams p) {
 #pragma unroll
     for (int k = 0; k < WN; ++k) {
       const int n = n0 + wave_n * 32 * WN + k * 32 + col;
-      if (n >= p.N) continue;
+      if (n >= N_b) continue;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int row = mt * MT + wave_m * 32 * WM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;

@@ -71,6 +71,15 @@ conv1d_mfma_f32(const ConvParams p) {
   const int gbase = n0 + p.off;
   const int half = lane >> 5;  // K index inside the MFMA (0/1)
   const int col = lane & 31;   // GEMM column inside a 32-wide tile
+  // ragged batches: this item's valid input / output extent
+  const int L_in_b = p.len_in ? p.len_in[b] : p.L_in;
+  int N_b = p.N;
+  if (p.len_out) {
+    const int lo = p.len_out[b];
+    N_b = UPS ? (lo > 0 ? (lo - 1 + p.ups_p) / p.ups_s + 1 : 0) : lo;
+  }
+  if (n0 >= N_b) return;  // whole tile past this utterance's end (block-uniform)
+  const int L_out_b = (UPS && p.len_out) ? p.len_out[b] : p.L_out;
 
   // ---- weight slab: async global -> LDS copy (global_load_lds_dwordx4) ----
   auto issue_w = [&](int c, float* Ws) {
@@ -94,8 +103,8 @@ conv1d_mfma_f32(const ConvParams p) {
       const int t = i - ci * XW;
       const int gi = gbase + t;
       const int cg = ci0 + ci;
-      const bool ok = (i < nx) && (cg < p.C_in) && ((unsigned)gi < (unsigned)p.L_in);
-      const int64_t idx = ok ? (int64_t)cg * p.L_in + gi : 0;
+      const bool ok = (i < nx) && (cg < p.C_in) && ((unsigned)gi < (unsigned)L_in_b);
+      const int64_t idx = ok ? (int64_t)cg * p.x_cs + (int64_t)gi * p.x_ts : 0;
       const float v = xb[idx];
       xv[q] = ok ? v : 0.f;
     }
@@ -191,7 +200,7 @@ conv1d_mfma_f32(const ConvParams p) {
 #pragma unroll
     for (int k = 0; k < WN; ++k) {
       const int n = n0 + wave_n * 32 * WN + k * 32 + col;
-      if (n >= p.N) continue;
+      if (n >= N_b) continue;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int row = mt * MT + wave_m * 32 * WM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
@@ -201,7 +210,7 @@ conv1d_mfma_f32(const ConvParams p) {
           const int co = row / p.ups_s;
           const int ph = row - co * p.ups_s;
           const int t = n * p.ups_s + ph - p.ups_p;
-          if (t >= 0 && t < p.L_out) p.y[(int64_t)b * p.y_bs + (int64_t)co * p.L_out + t] = v;
+          if (t >= 0 && t < L_out_b) p.y[(int64_t)b * p.y_bs + (int64_t)co * p.L_out + t] = v;
         } else {
           const int64_t o = (int64_t)b * p.y_bs + (int64_t)row * p.N + n;
           if (p.res) v = p.res[o] + v;  // x + conv2(...)   models/hifigan.py:85
@@ -223,7 +232,8 @@ conv1d_mfma_f32(const ConvParams p) {
 // a 256-sample tile of all C input rows staged in LDS.
 __global__ void __launch_bounds__(256)
 conv_post_tanh(const float* __restrict__ x, int64_t x_bs, int C, int L, const float* __restrict__ w,
-               const float* __restrict__ bias, float* __restrict__ wav) {
+               const float* __restrict__ bias, float* __restrict__ wav,
+               const int32_t* __restrict__ lens) {
   constexpr int TT = 256, KP = 7, HALO = 3;
   constexpr int XW = TT + KP - 1;
   extern __shared__ __attribute__((aligned(16))) float lds[];
@@ -232,18 +242,28 @@ conv_post_tanh(const float* __restrict__ x, int64_t x_bs, int C, int L, const fl
   const int t0 = blockIdx.x * TT;
   const int b = blockIdx.y;
   const float* xb = x + (int64_t)b * x_bs;
+  const int Lb = lens ? lens[b] : L;
+  if (t0 >= Lb) {  // past this utterance's end: zeros
+    const int t = t0 + threadIdx.x;
+    if (t < L) wav[(int64_t)b * L + t] = 0.f;
+    return;
+  }
   for (int i = threadIdx.x; i < C * KP; i += TT) Ws[i] = w[i];
   for (int c = 0; c < C; ++c) {
     for (int t = threadIdx.x; t < XW; t += TT) {
       const int gi = t0 - HALO + t;
       float v = 0.f;
-      if (gi >= 0 && gi < L) v = lrelu(xb[(int64_t)c * L + gi]);
+      if (gi >= 0 && gi < Lb) v = lrelu(xb[(int64_t)c * L + gi]);
       Xs[c * XW + t] = v;
     }
   }
   __syncthreads();
   const int t = t0 + threadIdx.x;
   if (t >= L) return;
+  if (t >= Lb) {
+    wav[(int64_t)b * L + t] = 0.f;
+    return;
+  }
   float acc = 0.f;
   for (int c = 0; c < C; ++c) {
     const float* xs = Xs + c * XW + threadIdx.x;
@@ -326,8 +346,8 @@ hipError_t launch_conv(TileId tile, int kt, bool ups, const ConvParams& p, int n
 }
 
 hipError_t launch_conv_post(const float* x, int64_t x_bs, int C, int L, const float* w,
-                            const float* bias, float* wav, int batch, hipStream_t stream,
-                            const char** name) {
+                            const float* bias, float* wav, const int32_t* lens, int batch,
+                            hipStream_t stream, const char** name) {
   const size_t lds = sizeof(float) * ((size_t)((C * 7 + 3) & ~3) + (size_t)C * (256 + 6));
   if (lds > 160 * 1024) return hipErrorInvalidValue;
   static bool attr = false;
@@ -339,7 +359,29 @@ hipError_t launch_conv_post(const float* x, int64_t x_bs, int C, int L, const fl
   }
   if (name) *name = "conv_post_tanh";
   dim3 grid((L + 255) / 256, batch);
-  conv_post_tanh<<<grid, dim3(256), lds, stream>>>(x, x_bs, C, L, w, bias, wav);
+  conv_post_tanh<<<grid, dim3(256), lds, stream>>>(x, x_bs, C, L, w, bias, wav, lens);
+  return hipGetLastError();
+}
+
+__global__ void stage_lengths_kernel(const int32_t* __restrict__ lens, int B, StageLenParams sp,
+                                     int32_t* __restrict__ out) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  int L = lens ? lens[b] : sp.T;
+  L = L < 0 ? 0 : (L > sp.T ? sp.T : L);
+  out[b] = L;
+  for (int s = 0; s < sp.n_up; ++s) {
+    const int u = sp.up_rates[s], k = sp.up_kernels[s];
+    const int d = k - u;
+    const int pad = d >= 0 ? d / 2 : -((-d + 1) / 2);  // Python floor division
+    L = L > 0 ? (L - 1) * u - 2 * pad + k : 0;
+    out[(s + 1) * B + b] = L;
+  }
+}
+
+hipError_t launch_stage_lengths(const int32_t* lens, int B, const StageLenParams& sp,
+                                int32_t* out, hipStream_t stream) {
+  stage_lengths_kernel<<<dim3((B + 255) / 256), dim3(256), 0, stream>>>(lens, B, sp, out);
   return hipGetLastError();
 }
 

@@ -406,8 +406,12 @@ Shapes shapes_for(const hfg_handle* h, int64_t B, int64_t T) {
   return s;
 }
 
+// 4 activation buffers + the per-stage length table of a ragged batch
+size_t lens_table_bytes(const hfg_handle* h, int64_t B) {
+  return (((size_t)(h->cfg.n_up + 1) * (size_t)B * sizeof(int32_t)) + 255) & ~(size_t)255;
+}
 size_t ws_bytes_for(const hfg_handle* h, int64_t B, int64_t T) {
-  return 4 * sizeof(float) * (size_t)shapes_for(h, B, T).buf_elems;
+  return 4 * sizeof(float) * (size_t)shapes_for(h, B, T).buf_elems + lens_table_bytes(h, B);
 }
 
 hipEvent_t pool_event(hfg_handle* h) {
@@ -451,12 +455,16 @@ struct Launcher {
 // One conv-layer launch (regular Conv1d).
 int run_conv(hfg_handle* h, Launcher& ln, const Layer& L, const float* x, int64_t B, int64_t Lt,
              float* y, bool act_in, bool act_out, const float* res, float* mrf, int mrf_mode,
-             float mrf_div) {
+             float mrf_div, const int32_t* lens, bool x_btc = false) {
   ConvParams p{};
   p.x = x;
   p.x_bs = (int64_t)L.C_in * Lt;
+  p.x_cs = x_btc ? 1 : Lt;          // [B][T][C] (acoustic-model layout) or [B][C][T]
+  p.x_ts = x_btc ? L.C_in : 1;
   p.C_in = L.C_in;
   p.L_in = (int)Lt;
+  p.len_in = lens;
+  p.len_out = lens;
   p.w = h->packed_dev + L.w_off;
   p.bias = h->packed_dev + L.b_off;
   p.y = y;
@@ -492,13 +500,17 @@ int run_conv(hfg_handle* h, Launcher& ln, const Layer& L, const float* x, int64_
 }
 
 int run_ups(hfg_handle* h, Launcher& ln, const Layer& L, const float* x, int64_t B, int64_t Lin,
-            int64_t Lout, float* y) {
+            int64_t Lout, float* y, const int32_t* len_in, const int32_t* len_out) {
   const TileCfg& t = kTiles[L.tile];
   ConvParams p{};
   p.x = x;
   p.x_bs = (int64_t)L.C_in * Lin;
+  p.x_cs = Lin;
+  p.x_ts = 1;
   p.C_in = L.C_in;
   p.L_in = (int)Lin;
+  p.len_in = len_in;
+  p.len_out = len_out;
   p.w = h->packed_dev + L.w_off;
   p.bias = h->packed_dev + L.b_off;
   p.y = y;
@@ -527,9 +539,13 @@ int run_ups(hfg_handle* h, Launcher& ln, const Layer& L, const float* x, int64_t
   return HFG_OK;
 }
 
-int forward_impl(hfg_handle* h, const float* mel, int64_t B, int64_t T, float* wav,
-                 int64_t out_len, void* ws, size_t ws_len, hipStream_t stream) {
+int forward_impl(hfg_handle* h, const float* mel, int64_t B, int64_t T, const hfg_forward_opts* o,
+                 float* wav, int64_t out_len, void* ws, size_t ws_len, hipStream_t stream) {
   if (!mel || !wav) return fail(HFG_EINVAL, "mel / wav pointer is NULL");
+  const bool btc = o && o->mel_layout == HFG_MEL_BTC;
+  if (o && o->mel_layout != HFG_MEL_BCT && o->mel_layout != HFG_MEL_BTC)
+    return fail(HFG_EINVAL, "unknown mel_layout %d", o->mel_layout);
+  const int32_t* user_lens = o ? o->lengths : nullptr;
   if (B <= 0 || T <= 0) return fail(HFG_EINVAL, "B and T must be > 0 (got %lld, %lld)",
                                     (long long)B, (long long)T);
   const Shapes sh = shapes_for(h, B, T);
@@ -550,16 +566,32 @@ int forward_impl(hfg_handle* h, const float* mel, int64_t B, int64_t T, float* w
   Launcher ln{h, stream};
   const hfg_config& c = h->cfg;
   int rc;
+  // ragged batch: per-stage valid lengths, computed on the device from lengths[B]
+  const int32_t* lt = nullptr;  // lt + s*B = lengths after s upsample stages
+  if (user_lens) {
+    int32_t* table = reinterpret_cast<int32_t*>(buf[3] + sh.buf_elems);
+    hfg::StageLenParams sp{};
+    sp.n_up = c.n_up;
+    sp.T = (int)T;
+    for (int i = 0; i < c.n_up; ++i) {
+      sp.up_rates[i] = c.up_rates[i];
+      sp.up_kernels[i] = c.up_kernels[i];
+    }
+    hipError_t e = hfg::launch_stage_lengths(user_lens, (int)B, sp, table, stream);
+    if (e != hipSuccess) return fail(HFG_EIO, "launch stage_lengths: %s", hipGetErrorString(e));
+    lt = table;
+  }
+  auto lens_at = [&](int s) { return lt ? lt + (size_t)s * B : nullptr; };
   // conv_pre  (models/hifigan.py:238)
   rc = run_conv(h, ln, h->layers[h->conv_pre], mel, B, T, R, false, false, nullptr, nullptr, 0,
-                1.f);
+                1.f, lens_at(0), btc);
   if (rc) return rc;
   const float* cur = R;
   for (int i = 0; i < c.n_up; ++i) {
     const Stage& st = h->stages[i];
     const int64_t Lin = sh.L[i], L = sh.L[i + 1];
     // lrelu -> ups[i]  (models/hifigan.py:244-245)
-    rc = run_ups(h, ln, h->layers[st.conv_ups], cur, B, Lin, L, X);
+    rc = run_ups(h, ln, h->layers[st.conv_ups], cur, B, Lin, L, X, lens_at(i), lens_at(i + 1));
     if (rc) return rc;
     // MRF (models/hifigan.py:116-131) of ResBlocks (:72-86)
     int idx = 0;
@@ -569,16 +601,18 @@ int forward_impl(hfg_handle* h, const float* mel, int64_t B, int64_t T, float* w
         const Layer& L1 = h->layers[st.conv1[idx]];
         const Layer& L2 = h->layers[st.conv2[idx]];
         // xt = lrelu(conv1(lrelu(x)))
-        rc = run_conv(h, ln, L1, src, B, L, Tb, true, true, nullptr, nullptr, 0, 1.f);
+        rc = run_conv(h, ln, L1, src, B, L, Tb, true, true, nullptr, nullptr, 0, 1.f,
+                      lens_at(i + 1));
         if (rc) return rc;
         const bool last = (m == c.n_dil[j] - 1);
         if (!last) {
           // x = x + conv2(xt)
-          rc = run_conv(h, ln, L2, Tb, B, L, R, false, false, src, nullptr, 0, 1.f);
+          rc = run_conv(h, ln, L2, Tb, B, L, R, false, false, src, nullptr, 0, 1.f,
+                        lens_at(i + 1));
         } else {
           int mode = (j > 0 ? 1 : 0) | (j == c.n_res - 1 ? 2 : 0);
           rc = run_conv(h, ln, L2, Tb, B, L, nullptr, false, false, src, MRF, mode,
-                        (float)c.n_res);
+                        (float)c.n_res, lens_at(i + 1));
         }
         if (rc) return rc;
       }
@@ -593,7 +627,7 @@ int forward_impl(hfg_handle* h, const float* mel, int64_t B, int64_t T, float* w
     ln.begin(2.0 * Lp.C_in * 7 * (double)L * B, 4.0 * B * L * (Lp.C_in + 1));
     hipError_t e = hfg::launch_conv_post(cur, (int64_t)Lp.C_in * L, Lp.C_in, (int)L,
                                          h->packed_dev + Lp.w_off, h->packed_dev + Lp.b_off, wav,
-                                         (int)B, stream, &name);
+                                         lens_at(c.n_up), (int)B, stream, &name);
     ln.end(name);
     if (e != hipSuccess) return fail(HFG_EIO, "launch conv_post: %s", hipGetErrorString(e));
   }
@@ -756,6 +790,22 @@ int hfg_reserve(hfg_handle* h, int64_t B, int64_t T) {
   return HFG_OK;
 }
 
+int hfg_forward_ex(hfg_handle* h, const float* mel, int64_t B, int64_t T,
+                   const hfg_forward_opts* opts, float* wav, int64_t out_len, void* workspace,
+                   size_t workspace_bytes, void* stream) {
+  if (!h) return fail(HFG_EINVAL, "handle is NULL");
+  if (h->device < 0) return fail(HFG_EINVAL, "host-only handle cannot run forward");
+  if (!workspace) return fail(HFG_EINVAL, "workspace is NULL");
+  DeviceGuard g(h->device);
+  if (!g.ok) return fail(HFG_ENODEV, "hipSetDevice(%d) failed", h->device);
+  if (h->dirty) {
+    int rc = do_commit(h);
+    if (rc) return rc;
+  }
+  return forward_impl(h, mel, B, T, opts, wav, out_len, workspace, workspace_bytes,
+                      reinterpret_cast<hipStream_t>(stream));
+}
+
 int hfg_forward_ws(hfg_handle* h, const float* mel, int64_t B, int64_t T, float* wav,
                    int64_t out_len, void* workspace, size_t workspace_bytes, void* stream) {
   if (!h) return fail(HFG_EINVAL, "handle is NULL");
@@ -767,7 +817,7 @@ int hfg_forward_ws(hfg_handle* h, const float* mel, int64_t B, int64_t T, float*
     int rc = do_commit(h);
     if (rc) return rc;
   }
-  return forward_impl(h, mel, B, T, wav, out_len, workspace, workspace_bytes,
+  return forward_impl(h, mel, B, T, nullptr, wav, out_len, workspace, workspace_bytes,
                       reinterpret_cast<hipStream_t>(stream));
 }
 

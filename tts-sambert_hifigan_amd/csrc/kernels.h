@@ -15,9 +15,12 @@ constexpr float kLReluSlope = 0.1f;  // F.leaky_relu(x, 0.1), models/hifigan.py:
 // Polyphase ConvTranspose1d (UPS): m = co*s + r and the result lands at
 // y[b][co][n*s + r - p].
 struct ConvParams {
-  const float* x;    // [B][C_in][L_in]
+  const float* x;    // [B][C_in][L_in] (or [B][L_in][C_in] for a BTC mel: see x_cs/x_ts)
   int64_t x_bs;      // batch stride of x (elements)
+  int64_t x_cs, x_ts;  // channel / time strides of x (L_in, 1 for [B][C][L])
   int C_in, L_in;
+  const int32_t* len_in;   // per-item valid input length (device, [B]) or null = L_in
+  const int32_t* len_out;  // per-item valid output length (device, [B]) or null = N / L_out
   const float* w;    // packed weights (see pack layout in hifigan_capi.cpp)
   const float* bias; // per GEMM row m, length >= m_tiles * MT
   float* y;          // output [B][M][N] (regular) or [B][C_out][L_out] (UPS)
@@ -101,8 +104,18 @@ hipError_t launch_conv(TileId tile, int kt, bool ups, const ConvParams& p, int n
                        int m_tiles, int batch, hipStream_t stream, const char** name);
 
 // conv_post + tanh: wav[b][t] = tanh(bias + sum_{c,j} w[c][j] * lrelu(x[b][c][t+j-3]))
+// for t < lens[b] (lens null = L); 0 beyond.
 hipError_t launch_conv_post(const float* x, int64_t x_bs, int C, int L, const float* w,
-                            const float* bias, float* wav, int batch, hipStream_t stream,
-                            const char** name);
+                            const float* bias, float* wav, const int32_t* lens, int batch,
+                            hipStream_t stream, const char** name);
+
+// Per-stage valid lengths of a ragged batch: out[s*B + b] = length after s
+// upsample stages of an utterance with lens[b] frames (clamped to [0, T]).
+struct StageLenParams {
+  int n_up, T;
+  int up_rates[8], up_kernels[8];
+};
+hipError_t launch_stage_lengths(const int32_t* lens, int B, const StageLenParams& sp,
+                                int32_t* out, hipStream_t stream);
 
 }  // namespace hfg

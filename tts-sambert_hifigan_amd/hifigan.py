@@ -167,11 +167,16 @@ class HiFiGANGenerator(nn.Module):
         return length
 
     # ------------------------------------------------------------------
-    def forward(self, mel: torch.Tensor) -> torch.Tensor:
+    def forward(self, mel: torch.Tensor, *, lengths=None, mel_layout: str = "bct") -> torch.Tensor:
         """Generate waveform from mel-spectrogram (models/hifigan.py:224-261).
 
         Args:
-            mel: [B, n_mels, Tfrm] float32 on a HIP device
+            mel: [B, n_mels, Tfrm] float32 on a HIP device ([B, Tfrm, n_mels] with
+                 ``mel_layout="btc"``, the acoustic model's output layout).
+            lengths: optional valid frames per utterance of a zero-padded batch
+                 (sequence of ints or an int tensor).  Item b's wav then equals the
+                 Generator run on mel[b, :, :lengths[b]] alone, zero past
+                 ``output_length(lengths[b])``.
         Returns:
             wav: [B, 1, T_wav] float32, T_wav = Tfrm * prod(upsample_rates)
         """
@@ -179,14 +184,18 @@ class HiFiGANGenerator(nn.Module):
             print(f"[HiFiGANGenerator] Input mel shape: {mel.shape}")
         if not isinstance(mel, torch.Tensor) or mel.dim() != 3:
             raise RuntimeError(f"expected mel [B, n_mels, T], got {getattr(mel, 'shape', type(mel))}")
-        if mel.shape[1] != self.n_mels:
-            raise RuntimeError(f"expected {self.n_mels} mel channels, got {mel.shape[1]}")
+        if mel_layout not in ("bct", "btc"):
+            raise ValueError("mel_layout must be 'bct' or 'btc'")
+        n_ch = mel.shape[1] if mel_layout == "bct" else mel.shape[2]
+        if n_ch != self.n_mels:
+            raise RuntimeError(f"expected {self.n_mels} mel channels, got {n_ch}")
         if not mel.is_cuda:
             raise RuntimeError("HiFiGANGenerator (MI355X) runs on the HIP device only; "
                                "move the mel to 'cuda' (there is no CPU fallback)")
         if torch.is_grad_enabled() and mel.requires_grad:
             raise NotImplementedError("inference-only HIP path: no autograd through the Generator")
-        B, _, T = mel.shape
+        B = mel.shape[0]
+        T = mel.shape[2] if mel_layout == "bct" else mel.shape[1]
         if B == 0 or T == 0:
             raise RuntimeError("empty mel input")
         mel_c = mel.detach().to(torch.float32).contiguous()
@@ -197,8 +206,19 @@ class HiFiGANGenerator(nn.Module):
             ws_bytes = h.workspace_bytes(B, T)
             ws = torch.empty(ws_bytes, dtype=torch.uint8, device=mel.device)
             stream = torch.cuda.current_stream(mel.device).cuda_stream
-            h.forward_ws(mel_c.data_ptr(), B, T, wav.data_ptr(), out_len, ws.data_ptr(), ws_bytes,
-                         stream)
+            if lengths is None and mel_layout == "bct":
+                h.forward_ws(mel_c.data_ptr(), B, T, wav.data_ptr(), out_len, ws.data_ptr(),
+                             ws_bytes, stream)
+            else:
+                lens_t = None
+                if lengths is not None:
+                    lens_t = torch.as_tensor(lengths).to(device=mel.device, dtype=torch.int32)
+                    if lens_t.shape != (B,):
+                        raise RuntimeError(f"lengths must have shape [{B}]")
+                    lens_t = lens_t.contiguous()
+                h.forward_ex(mel_c.data_ptr(), B, T, wav.data_ptr(), out_len, ws.data_ptr(),
+                             ws_bytes, stream, mel_layout=mel_layout,
+                             lengths_ptr=lens_t.data_ptr() if lens_t is not None else 0)
         if self.debug_shapes:
             x_len = T
             c = self.conv_pre.out_channels
@@ -211,6 +231,27 @@ class HiFiGANGenerator(nn.Module):
                 print(f"[HiFiGANGenerator] After MRF {i}: {torch.Size([B, c, x_len])}")
             print(f"[HiFiGANGenerator] Output wav shape: {wav.shape}")
         return wav
+
+    def receptive_field_frames(self) -> int:
+        """Upper bound, in mel frames, of how far (each side) an output sample's
+        value depends on the input: conv_pre + per-stage upsampler and MRF halos
+        + conv_post, each divided by the stage's samples-per-frame.  A chunk with
+        this many context frames on both sides reproduces the full-length run."""
+        rate = 1
+        halo = 3.0  # conv_pre k=7
+        for up, mrf in zip(self.ups, self.mrfs):
+            u, k = up.stride[0], up.kernel_size[0]
+            halo += -(-k // u) / rate  # taps per output phase, in input samples
+            rate *= u
+            best = 0
+            for rb in mrf.resblocks:
+                s = 0
+                for c1, c2 in zip(rb.convs1, rb.convs2):
+                    s += c1.padding[0] + c2.padding[0]
+                best = max(best, s)
+            halo += best / rate
+        halo += 3.0 / rate  # conv_post k=7
+        return int(halo) + 1
 
     def remove_weight_norm(self):
         """models/hifigan.py:263-272"""
