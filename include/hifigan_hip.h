@@ -158,6 +158,37 @@ int hfg_set_profiling(hfg_handle* h, int enable);
 int hfg_profile_reset(hfg_handle* h);
 int hfg_profile_summary(hfg_handle* h, char* buf, size_t buflen);
 
+/* ---------------------------------------------------------------------------
+ * On-device log-mel framing feeding the vocoder:
+ * replaces extract_mel's MelSpectrogram + log (data/audio_processing.py:98-133;
+ * the same framing as VocoderLoss.mel_transform, models/losses.py:414-426).
+ * wav [B][n_samples] fp32 -> mel [B][n_mels][n_samples/hop + 1] (center=True,
+ * reflect pad, periodic Hann, power 2, mel filterbank, log).
+ * ------------------------------------------------------------------------- */
+typedef struct hfg_mel_handle hfg_mel_handle;
+typedef struct hfg_mel_config {
+    int32_t sample_rate;   /* 22050 (config.yaml:5)          */
+    int32_t n_fft;         /* 1024                           */
+    int32_t hop_length;    /* 256                            */
+    int32_t win_length;    /* 1024                           */
+    int32_t n_mels;        /* 80                             */
+    float f_min, f_max;    /* 0, 8000                        */
+    int32_t mel_scale;     /* 0 = slaney, 1 = htk            */
+    int32_t norm;          /* 0 = none, 1 = slaney           */
+    float log_eps;         /* 1e-10 (audio_processing.py:123) */
+    int32_t log_base;      /* 10 = log10, 0 = natural log    */
+} hfg_mel_config;
+
+const char* hfg_mel_last_error(void);
+int hfg_mel_create(const hfg_mel_config* cfg, int device, hfg_mel_handle** out);
+void hfg_mel_destroy(hfg_mel_handle* h);
+/* the [n_fft/2+1][n_mels] filterbank (torchaudio melscale_fbanks), host side */
+int hfg_mel_filterbank(const hfg_mel_config* cfg, float* out);
+int64_t hfg_mel_frames(const hfg_mel_handle* h, int64_t n_samples);
+size_t hfg_mel_workspace_bytes(const hfg_mel_handle* h, int64_t B, int64_t n_samples);
+int hfg_mel_forward(hfg_mel_handle* h, const float* wav, int64_t B, int64_t n_samples,
+                    float* mel, void* workspace, size_t workspace_bytes, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

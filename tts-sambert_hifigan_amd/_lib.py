@@ -95,6 +95,13 @@ def make_config(n_mels, upsample_rates, upsample_kernel_sizes, upsample_initial_
     return c
 
 
+class HfgMelConfig(ctypes.Structure):
+    _fields_ = [("sample_rate", c_int32), ("n_fft", c_int32), ("hop_length", c_int32),
+                ("win_length", c_int32), ("n_mels", c_int32), ("f_min", c_float),
+                ("f_max", c_float), ("mel_scale", c_int32), ("norm", c_int32),
+                ("log_eps", c_float), ("log_base", c_int32)]
+
+
 _lib = None
 
 # name -> (restype, argtypes); every symbol declared in include/hifigan_hip*.h
@@ -119,6 +126,14 @@ SIGNATURES = {
     "hfg_profile_summary": (c_int, [c_void_p, c_char_p, c_size_t]),
     "hfg_debug_packed_layer": (c_int, [c_void_p, c_char_p, POINTER(c_float), c_size_t,
                                        POINTER(c_int64)]),
+    "hfg_mel_last_error": (c_char_p, []),
+    "hfg_mel_create": (c_int, [POINTER(HfgMelConfig), c_int, POINTER(c_void_p)]),
+    "hfg_mel_destroy": (None, [c_void_p]),
+    "hfg_mel_filterbank": (c_int, [POINTER(HfgMelConfig), POINTER(c_float)]),
+    "hfg_mel_frames": (c_int64, [c_void_p, c_int64]),
+    "hfg_mel_workspace_bytes": (c_size_t, [c_void_p, c_int64, c_int64]),
+    "hfg_mel_forward": (c_int, [c_void_p, c_void_p, c_int64, c_int64, c_void_p, c_void_p,
+                                c_size_t, c_void_p]),
 }
 
 
