@@ -14,7 +14,7 @@ LIB_NAME = "libhifigan_hip.so"
 LIB_PATH = os.path.join(PKG_DIR, LIB_NAME)
 SOURCES = ["conv_kernels.hip", "conv_bf16x3.hip", "hifigan_capi.cpp", "mel_kernels.hip",
            "mel_capi.cpp"]
-HEADERS = ["kernels.h", "mel_kernels.h", os.path.join("..", "..", "include", "hifigan_hip.h"),
+HEADERS = ["kernels.h", "mel_kernels.h", "epilogue.h", os.path.join("..", "..", "include", "hifigan_hip.h"),
            os.path.join("..", "..", "include", "hifigan_hip_inspect.h")]
 
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")

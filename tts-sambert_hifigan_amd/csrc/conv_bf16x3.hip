@@ -22,11 +22,12 @@
 
 #include <cstdio>
 
+#include "epilogue.h"
 #include "kernels.h"
 
 namespace hfg {
 
-typedef float floatx16 __attribute__((ext_vector_type(16)));
+typedef floatx16e floatx16;
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __attribute__((address_space(3))) void* lds_ptr_t3;
 typedef __attribute__((address_space(1))) void* gptr_t1;
@@ -43,15 +44,19 @@ conv1d_bf16x3(const ConvParams p) {
   constexpr int XROW = 24;                        // bf16 per staged row: 16 ch + 8 pad (48 B)
   constexpr int TAP_ELEMS = 2 * WAVES_M * WM * 64 * 8;  // bf16 per tap of a slab (hi+lo)
   constexpr int SLAB = TPC * TAP_ELEMS;           // bf16 per chunk slab
-  constexpr int XW_MAX = NTILE + (TPC - 1) * kMaxDil;
+  constexpr int KT_MAX = KT_ > 0 ? KT_ : 16;
+  constexpr int XW_MAX = NTILE + (KT_MAX - 1) * kMaxDil;
   constexpr int XQ = (2 * XW_MAX + NT - 1) / NT;  // staging tasks per thread
   const int KT = KT_ > 0 ? KT_ : p.kt;
   const int n_tg = (KT + TPC - 1) / TPC;          // tap groups per channel group
-  const int XW = NTILE + (TPC - 1) * p.dil;       // staged rows per chunk
-  const int xplane = XW * XROW;                   // bf16 per X plane
-  const int stage_elems = SLAB + 2 * ((xplane + 7) & ~7);
+  // one staged input window per 16-channel group serves all KT taps
+  const int XW = NTILE + (KT - 1) * p.dil;
+  const int xplane = (XW * XROW + 7) & ~7;        // bf16 per X plane
+  const int xbuf = 2 * xplane;                    // hi + lo planes
 
   extern __shared__ __attribute__((aligned(16))) __bf16 lds16[];
+  __bf16* const Wbuf0 = lds16;
+  __bf16* const Xbuf0 = lds16 + 2 * SLAB;
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -69,6 +74,8 @@ conv1d_bf16x3(const ConvParams p) {
   const int L_in_b = p.len_in ? p.len_in[b] : p.L_in;
   const int N_b = p.len_out ? p.len_out[b] : p.N;
   if (n0 >= N_b) return;  // whole tile past this utterance's end (block-uniform)
+  const int xcs = (int)p.x_cs, xts = (int)p.x_ts;
+  const int wbase = n0 + p.off;                   // input index of window row 0
 
   auto taps_in = [&](int c) {
     const int tg = c % n_tg;
@@ -86,29 +93,30 @@ conv1d_bf16x3(const ConvParams p) {
                                          16, 0, 0);
     }
   };
-  // ---- activations: 8 channels of one time step per task, in registers ----
+  // ---- activations: task = (window row t, 8 channels), 32-bit offsets from xb ----
   float xv[XQ][8];
-  auto load_x = [&](int c) {
-    const int g = c / n_tg, tg = c % n_tg;
-    const int ws = n0 + p.off + tg * TPC * p.dil;
+  auto load_x = [&](int g) {
+    const bool full = g * 16 + 16 <= p.C_in;  // block-uniform
 #pragma unroll
     for (int q = 0; q < XQ; ++q) {
       const int i = tid + q * NT;
       const int t = i >> 1;
       const int cb = g * 16 + (i & 1) * 8;
-      const int gi = ws + t;
+      const int gi = wbase + t;
       const bool tok = (i < 2 * XW) && ((unsigned)gi < (unsigned)L_in_b);
+      // byte offsets from the block-uniform base: SGPR base + 32-bit VGPR offset loads
+      const unsigned o0 = tok ? (unsigned)(cb * xcs + gi * xts) * 4u : 0u;
+      const unsigned step = tok ? (unsigned)xcs * 4u : 0u;
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
-        const bool ok = tok && (cb + e < p.C_in);
-        const int64_t idx = ok ? (int64_t)(cb + e) * p.x_cs + (int64_t)gi * p.x_ts : 0;
-        const float v = xb[idx];
+        const bool ok = tok && (full || cb + e < p.C_in);
+        const float v = *reinterpret_cast<const float*>(reinterpret_cast<const char*>(xb) + (o0 + e * step));
         xv[q][e] = ok ? v : 0.f;
       }
     }
   };
   auto store_x = [&](__bf16* Xh) {
-    __bf16* Xl = Xh + ((xplane + 7) & ~7);
+    __bf16* Xl = Xh + xplane;
 #pragma unroll
     for (int q = 0; q < XQ; ++q) {
       const int i = tid + q * NT;
@@ -140,17 +148,18 @@ conv1d_bf16x3(const ConvParams p) {
   struct Frag {
     bf16x8 ah[WM], al[WM], bh[WN], bl[WN];
   };
-  auto load_frag = [&](const __bf16* Ws, const __bf16* Xh, int jj, Frag& f) {
-    const __bf16* Xl = Xh + ((xplane + 7) & ~7);
+  // jj: tap inside the chunk's slab; tap: tap index inside the window
+  auto load_frag = [&](const __bf16* Ws, const __bf16* Xh, int jj, int tap, Frag& f) {
+    const __bf16* Xl = Xh + xplane;
 #pragma unroll
     for (int i = 0; i < WM; ++i) {
-      const __bf16* a = Ws + jj * TAP_ELEMS + ((0 * WAVES_M + wave_m) * WM + i) * 512 + lane * 8;
+      const __bf16* a = Ws + jj * TAP_ELEMS + (wave_m * WM + i) * 512 + lane * 8;
       f.ah[i] = *reinterpret_cast<const bf16x8*>(a);
       f.al[i] = *reinterpret_cast<const bf16x8*>(a + WAVES_M * WM * 512);
     }
 #pragma unroll
     for (int k = 0; k < WN; ++k) {
-      const int t = wave_n * 32 * WN + k * 32 + col + jj * p.dil;
+      const int t = wave_n * 32 * WN + k * 32 + col + tap * p.dil;
       const int off = t * XROW + half * 8;
       f.bh[k] = *reinterpret_cast<const bf16x8*>(Xh + off);
       f.bl[k] = *reinterpret_cast<const bf16x8*>(Xl + off);
@@ -167,64 +176,45 @@ conv1d_bf16x3(const ConvParams p) {
       }
   };
 
-  // ---- prologue ----
-  issue_w(0, lds16);
+  // ---- prologue: weight slab of chunk 0, input window of channel group 0 ----
+  issue_w(0, Wbuf0);
   load_x(0);
-  store_x(lds16 + SLAB);
+  store_x(Xbuf0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
+  // chunk c = (channel group g, tap group tg); weights double-buffered per chunk,
+  // the input window double-buffered per channel group (staged once for all taps)
   for (int c = 0; c < p.n_chunks; ++c) {
-    __bf16* Ws = lds16 + (c & 1) * stage_elems;
-    __bf16* Xh = Ws + SLAB;
-    __bf16* Wn = lds16 + ((c + 1) & 1) * stage_elems;
+    const int g = c / n_tg, tg = c - (c / n_tg) * n_tg;
+    const __bf16* Ws = Wbuf0 + (c & 1) * SLAB;
+    const __bf16* Xh = Xbuf0 + (g & 1) * xbuf;
     const bool has_next = c + 1 < p.n_chunks;
-    if (has_next) {
-      issue_w(c + 1, Wn);
-      load_x(c + 1);
-    }
+    const bool next_group = has_next && tg == n_tg - 1;
+    if (has_next && !(p.dbg & 2)) issue_w(c + 1, Wbuf0 + ((c + 1) & 1) * SLAB);
+    const bool stage_x = next_group && !(p.dbg & 1);
+    if (stage_x) load_x(g + 1);
     const int nt = taps_in(c);
+    const int tap0 = tg * TPC;
     Frag f0, f1;
-    load_frag(Ws, Xh, 0, f0);
+    load_frag(Ws, Xh, 0, tap0, f0);
 #pragma unroll
     for (int jj = 0; jj < TPC; jj += 2) {
       if (jj < nt) {
-        if (jj + 1 < nt) load_frag(Ws, Xh, jj + 1, f1);
+        if (jj + 1 < nt) load_frag(Ws, Xh, jj + 1, tap0 + jj + 1, f1);
         mma(f0);
-        if (jj + 2 < nt) load_frag(Ws, Xh, jj + 2, f0);
+        if (jj + 2 < nt) load_frag(Ws, Xh, jj + 2, tap0 + jj + 2, f0);
         if (jj + 1 < nt) mma(f1);
       }
     }
-    if (has_next) store_x(Wn + SLAB);
+    if (stage_x) store_x(Xbuf0 + ((g + 1) & 1) * xbuf);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }
 
   // ---- epilogue (same contract as conv1d_mfma_f32) ----
-#pragma unroll
-  for (int i = 0; i < WM; ++i) {
-#pragma unroll
-    for (int k = 0; k < WN; ++k) {
-      const int n = n0 + wave_n * 32 * WN + k * 32 + col;
-      if (n >= N_b) continue;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int row = mt * MT + wave_m * 32 * WM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
-        if (row >= p.M) continue;
-        float v = acc[i][k][r] + p.bias[row];
-        const int64_t o = (int64_t)b * p.y_bs + (int64_t)row * p.N + n;
-        if (p.res) v = p.res[o] + v;
-        if (p.act_out) v = lrelu3(v);
-        if (p.mrf) {
-          float m = (p.mrf_mode & 1) ? p.mrf[o] + v : v;
-          if (p.mrf_mode & 2) m = m / p.mrf_div;
-          p.mrf[o] = m;
-        } else {
-          p.y[o] = v;
-        }
-      }
-    }
-  }
+  conv_epilogue<WM, WN>(p, acc, b, mt * MT + wave_m * 32 * WM, n0 + wave_n * 32 * WN, N_b, half,
+                        col);
 }
 
 namespace {
@@ -257,12 +247,12 @@ Entry3 g_entries3[] = {
 
 }  // namespace
 
-size_t bf16x3_lds_bytes(int tile, int dil) {
+size_t bf16x3_lds_bytes(int tile, int kt, int dil) {
   const Bf16x3Cfg& t = kBf16x3Tiles[tile];
   const size_t slab = (size_t)kBf16x3Tpc * 2 * t.MT() * 16;  // bf16: taps x planes x rows x 16 ch
-  const int xw = t.NTILE() + (kBf16x3Tpc - 1) * dil;
+  const int xw = t.NTILE() + (kt - 1) * dil;
   const size_t xplane = ((size_t)xw * 24 + 7) & ~(size_t)7;
-  return 2 * sizeof(__bf16) * (slab + 2 * xplane);
+  return sizeof(__bf16) * (2 * slab + 2 * 2 * xplane);  // 2 weight slabs + 2 (hi,lo) windows
 }
 
 hipError_t launch_conv_bf16x3(int tile, int kt, const ConvParams& p, int n_tiles, int m_tiles,
@@ -276,12 +266,12 @@ hipError_t launch_conv_bf16x3(int tile, int kt, const ConvParams& p, int n_tiles
   }
   if (!e) e = generic;
   if (!e) return hipErrorInvalidValue;
-  if (p.dil > kMaxDil) return hipErrorInvalidValue;
+  if (p.dil > kMaxDil || (e->kt == 0 && kt > 16)) return hipErrorInvalidValue;
   const Bf16x3Cfg& t = kBf16x3Tiles[tile];
   if (!e->name[0])
     snprintf(e->name, sizeof(e->name), "conv1d_bf16x3<%d, %d, %d, %d, %d, %d>", e->kt, kBf16x3Tpc,
              t.WAVES_M, t.WAVES_N, t.WM, t.WN);
-  const size_t lds = bf16x3_lds_bytes(tile, p.dil);
+  const size_t lds = bf16x3_lds_bytes(tile, kt, p.dil);
   if (lds > 160 * 1024) return hipErrorInvalidValue;
   if (!e->attr) {
     hipError_t err = hipFuncSetAttribute(reinterpret_cast<const void*>(e->fn),

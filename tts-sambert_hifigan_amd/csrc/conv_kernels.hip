@@ -28,11 +28,12 @@
 
 #include <cstdio>
 
+#include "epilogue.h"
 #include "kernels.h"
 
 namespace hfg {
 
-typedef float floatx16 __attribute__((ext_vector_type(16)));
+typedef floatx16e floatx16;
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 typedef __attribute__((address_space(1))) void* gptr_t;
 
@@ -104,8 +105,9 @@ conv1d_mfma_f32(const ConvParams p) {
       const int gi = gbase + t;
       const int cg = ci0 + ci;
       const bool ok = (i < nx) && (cg < p.C_in) && ((unsigned)gi < (unsigned)L_in_b);
-      const int64_t idx = ok ? (int64_t)cg * p.x_cs + (int64_t)gi * p.x_ts : 0;
-      const float v = xb[idx];
+      // byte offset from the block-uniform base (SGPR base + 32-bit VGPR offset load)
+      const unsigned boff = ok ? (unsigned)(cg * (int)p.x_cs + gi * (int)p.x_ts) * 4u : 0u;
+      const float v = *reinterpret_cast<const float*>(reinterpret_cast<const char*>(xb) + boff);
       xv[q] = ok ? v : 0.f;
     }
   };
@@ -195,36 +197,28 @@ conv1d_mfma_f32(const ConvParams p) {
   }
 
   // ---- epilogue ----
+  if constexpr (UPS) {
 #pragma unroll
-  for (int i = 0; i < WM; ++i) {
+    for (int i = 0; i < WM; ++i) {
 #pragma unroll
-    for (int k = 0; k < WN; ++k) {
-      const int n = n0 + wave_n * 32 * WN + k * 32 + col;
-      if (n >= N_b) continue;
+      for (int k = 0; k < WN; ++k) {
+        const int n = n0 + wave_n * 32 * WN + k * 32 + col;
+        if (n >= N_b) continue;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int row = mt * MT + wave_m * 32 * WM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
-        if (row >= p.M) continue;
-        float v = acc[i][k][r] + p.bias[row];
-        if constexpr (UPS) {
+        for (int r = 0; r < 16; ++r) {
+          const int row = mt * MT + wave_m * 32 * WM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
+          if (row >= p.M) continue;
+          const float v = acc[i][k][r] + p.bias[row];
           const int co = row / p.ups_s;
           const int ph = row - co * p.ups_s;
           const int t = n * p.ups_s + ph - p.ups_p;
           if (t >= 0 && t < L_out_b) p.y[(int64_t)b * p.y_bs + (int64_t)co * p.L_out + t] = v;
-        } else {
-          const int64_t o = (int64_t)b * p.y_bs + (int64_t)row * p.N + n;
-          if (p.res) v = p.res[o] + v;  // x + conv2(...)   models/hifigan.py:85
-          if (p.act_out) v = lrelu(v);
-          if (p.mrf) {
-            float m = (p.mrf_mode & 1) ? p.mrf[o] + v : v;   // output + resblock(x)  :129
-            if (p.mrf_mode & 2) m = m / p.mrf_div;            // output / len(...)     :131
-            p.mrf[o] = m;
-          } else {
-            p.y[o] = v;
-          }
         }
       }
     }
+  } else {
+    conv_epilogue<WM, WN>(p, acc, b, mt * MT + wave_m * 32 * WM, n0 + wave_n * 32 * WN, N_b,
+                          half, col);
   }
 }
 

@@ -9,6 +9,7 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <string>
@@ -94,6 +95,7 @@ struct hfg_handle {
   void* ws = nullptr;
   size_t ws_bytes = 0;
   bool profiling = false;
+  int dbg_flags = 0;  // HFG_DEBUG_FLAGS env (kernel ablations; wrong results when set)
   std::vector<ProfRec> prof;
   std::vector<hipEvent_t> event_pool;
 };
@@ -481,6 +483,7 @@ int run_conv(hfg_handle* h, Launcher& ln, const Layer& L, const float* x, int64_
   p.mrf_mode = mrf_mode;
   p.mrf_div = mrf_div;
   p.n_chunks = L.n_chunks;
+  p.dbg = h->dbg_flags;
   const int ntile = L.prec == 1 ? hfg::kBf16x3Tiles[L.tile].NTILE() : kTiles[L.tile].NTILE();
   const int n_tiles = (int)((Lt + ntile - 1) / ntile);
   const double flop = 2.0 * L.C_out * L.C_in * L.k * (double)Lt * B;
@@ -660,6 +663,7 @@ int hfg_create(const hfg_config* cfg, int device, hfg_handle** out) {
   if (!h) return fail(HFG_ENOMEM, "out of host memory");
   h->cfg = *cfg;
   h->device = device;
+  if (const char* dbg = getenv("HFG_DEBUG_FLAGS")) h->dbg_flags = atoi(dbg);
   build_layers(h);
   *out = h;
   return HFG_OK;

@@ -36,6 +36,8 @@ struct ConvParams {
   float mrf_div;
   int ups_s, ups_p, L_out;  // UPS store mapping
   int n_chunks;      // ceil(C_in / CK)
+  int dbg;           // ablation flags (HFG_DEBUG_FLAGS; 0 in production): bit0 skip input
+                     // restaging after the first chunk, bit1 skip weight restaging
 };
 
 // Tile configurations of conv1d_mfma_f32 (fp32 MFMA 32x32x2).
@@ -94,7 +96,7 @@ constexpr Bf16x3Cfg kBf16x3Tiles[kBf16x3Tiles_n] = {{2, 4, 2, 2}, {1, 8, 2, 1}};
 constexpr int kBf16x3Tpc = 4;  // taps per chunk (chunk = 16 channels x 4 taps)
 constexpr int kBf16x3Ck = 16;  // channels per chunk (one MFMA k-step per tap)
 inline int bf16x3_tile_for_rows(int M) { return M >= 128 ? 0 : (M >= 64 ? 1 : -1); }
-size_t bf16x3_lds_bytes(int tile, int dil);
+size_t bf16x3_lds_bytes(int tile, int kt, int dil);
 hipError_t launch_conv_bf16x3(int tile, int kt, const ConvParams& p, int n_tiles, int m_tiles,
                               int batch, hipStream_t stream, const char** name);
 
