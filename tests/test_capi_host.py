@@ -216,19 +216,18 @@ def test_bf16x3_packing(pkg, preset):
     for k, v in sd.items():
         h.set_weight(k, torch.from_numpy(v))
     h.commit()
-    WAVES = {0: (2, 2), 1: (1, 2)}  # tile -> (WAVES_M, WM) of kBf16x3Tiles
-    TPC = 4
+    WAVES = {0: (2, 2, 4), 1: (1, 2, 2), 2: (1, 1, 4)}  # tile -> (WAVES_M, WM, TPC)
     n_checked = 0
     for mod in ["conv_pre", "mrfs.0.resblocks.2.convs1.1", "mrfs.1.resblocks.0.convs2.1",
                 "mrfs.2.resblocks.1.convs1.0", "mrfs.3.resblocks.2.convs2.1"]:
         info, packed, bias = h.packed_layer(mod)
         W = sd[mod + ".weight"]
         cout, cin, k = W.shape
-        if info["CK"] != 16:  # fp32 layer (C < 64 stage)
-            assert cout < 64
+        if info["CK"] != 16:  # fp32 layer (C < 32 stage)
+            assert cout < 32
             continue
         n_checked += 1
-        wm_, WM = WAVES[info["tile"]]
+        wm_, WM, TPC = WAVES[info["tile"]]
         MT = info["MT"]
         n_g, n_tg = -(-cin // 16), -(-k // TPC)
         assert info["n_chunks"] == n_g * n_tg

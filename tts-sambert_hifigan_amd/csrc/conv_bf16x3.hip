@@ -41,7 +41,7 @@ conv1d_bf16x3(const ConvParams p) {
   constexpr int NT = 64 * NW;
   constexpr int MT = 32 * WM * WAVES_M;
   constexpr int NTILE = 32 * WN * WAVES_N;
-  constexpr int XROW = 24;                        // bf16 per staged row: 16 ch + 8 pad (48 B)
+  constexpr int XROW = 16;  // bf16 per staged row: 16 channels (32 B), 16-B halves XOR-swizzled
   constexpr int TAP_ELEMS = 2 * WAVES_M * WM * 64 * 8;  // bf16 per tap of a slab (hi+lo)
   constexpr int SLAB = TPC * TAP_ELEMS;           // bf16 per chunk slab
   constexpr int KT_MAX = KT_ > 0 ? KT_ : 16;
@@ -130,7 +130,8 @@ conv1d_bf16x3(const ConvParams p) {
           h[e] = hh;
           l[e] = (__bf16)(v - (float)hh);
         }
-        const int off = (i >> 1) * XROW + (i & 1) * 8;
+        const int t = i >> 1;
+        const int off = t * XROW + 8 * ((i & 1) ^ ((t >> 3) & 1));  // swizzled half
         *reinterpret_cast<bf16x8*>(Xh + off) = h;
         *reinterpret_cast<bf16x8*>(Xl + off) = l;
       }
@@ -160,7 +161,8 @@ conv1d_bf16x3(const ConvParams p) {
 #pragma unroll
     for (int k = 0; k < WN; ++k) {
       const int t = wave_n * 32 * WN + k * 32 + col + tap * p.dil;
-      const int off = t * XROW + half * 8;
+      // rows t..t+31 of one half-wave: (t mod 16) distinct -> conflict-free ds_read_b128
+      const int off = t * XROW + 8 * (half ^ ((t >> 3) & 1));
       f.bh[k] = *reinterpret_cast<const bf16x8*>(Xh + off);
       f.bl[k] = *reinterpret_cast<const bf16x8*>(Xl + off);
     }
@@ -225,7 +227,7 @@ template <int KT, int TILE>
 struct Inst3 {
   static constexpr Bf16x3Cfg t = kBf16x3Tiles[TILE];
   static ConvFn3 fn() {
-    return conv1d_bf16x3<KT, kBf16x3Tpc, t.WAVES_M, t.WAVES_N, t.WM, t.WN>;
+    return conv1d_bf16x3<KT, t.TPC, t.WAVES_M, t.WAVES_N, t.WM, t.WN>;
   }
 };
 
@@ -243,15 +245,16 @@ struct Entry3 {
 Entry3 g_entries3[] = {
     HFG3_ENTRY(3, 0), HFG3_ENTRY(5, 0), HFG3_ENTRY(7, 0), HFG3_ENTRY(11, 0), HFG3_ENTRY(0, 0),
     HFG3_ENTRY(3, 1), HFG3_ENTRY(5, 1), HFG3_ENTRY(7, 1), HFG3_ENTRY(11, 1), HFG3_ENTRY(0, 1),
+    HFG3_ENTRY(3, 2), HFG3_ENTRY(5, 2), HFG3_ENTRY(7, 2), HFG3_ENTRY(11, 2), HFG3_ENTRY(0, 2),
 };
 
 }  // namespace
 
 size_t bf16x3_lds_bytes(int tile, int kt, int dil) {
   const Bf16x3Cfg& t = kBf16x3Tiles[tile];
-  const size_t slab = (size_t)kBf16x3Tpc * 2 * t.MT() * 16;  // bf16: taps x planes x rows x 16 ch
+  const size_t slab = (size_t)t.TPC * 2 * t.MT() * 16;  // bf16: taps x planes x rows x 16 ch
   const int xw = t.NTILE() + (kt - 1) * dil;
-  const size_t xplane = ((size_t)xw * 24 + 7) & ~(size_t)7;
+  const size_t xplane = ((size_t)xw * 16 + 7) & ~(size_t)7;
   return sizeof(__bf16) * (2 * slab + 2 * 2 * xplane);  // 2 weight slabs + 2 (hi,lo) windows
 }
 
@@ -269,7 +272,7 @@ hipError_t launch_conv_bf16x3(int tile, int kt, const ConvParams& p, int n_tiles
   if (p.dil > kMaxDil || (e->kt == 0 && kt > 16)) return hipErrorInvalidValue;
   const Bf16x3Cfg& t = kBf16x3Tiles[tile];
   if (!e->name[0])
-    snprintf(e->name, sizeof(e->name), "conv1d_bf16x3<%d, %d, %d, %d, %d, %d>", e->kt, kBf16x3Tpc,
+    snprintf(e->name, sizeof(e->name), "conv1d_bf16x3<%d, %d, %d, %d, %d, %d>", e->kt, t.TPC,
              t.WAVES_M, t.WAVES_N, t.WM, t.WN);
   const size_t lds = bf16x3_lds_bytes(tile, kt, p.dil);
   if (lds > 160 * 1024) return hipErrorInvalidValue;

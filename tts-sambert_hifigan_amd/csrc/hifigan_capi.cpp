@@ -221,14 +221,14 @@ void build_layers(hfg_handle* h) {
     }
     if (h->cfg.dtype == HFG_DTYPE_BF16X3 && L.kind == L_CONV &&
         hfg::bf16x3_tile_for_rows(L.M) >= 0) {
-      // split-precision path: chunk = 16 channels x kBf16x3Tpc taps
+      // split-precision path: chunk = 16 channels x TPC taps
       const hfg::Bf16x3Cfg& t3 = hfg::kBf16x3Tiles[hfg::bf16x3_tile_for_rows(L.M)];
       L.prec = 1;
       L.tile = hfg::bf16x3_tile_for_rows(L.M);
       L.CK = hfg::kBf16x3Ck;
       L.m_tiles = (L.M + t3.MT() - 1) / t3.MT();
-      L.n_chunks = ((L.C_in + L.CK - 1) / L.CK) * ((L.KT + hfg::kBf16x3Tpc - 1) / hfg::kBf16x3Tpc);
-      const size_t slab_bf16 = (size_t)hfg::kBf16x3Tpc * 2 * t3.MT() * 16;
+      L.n_chunks = ((L.C_in + L.CK - 1) / L.CK) * ((L.KT + t3.TPC - 1) / t3.TPC);
+      const size_t slab_bf16 = (size_t)t3.TPC * 2 * t3.MT() * 16;
       L.w_off = off;
       L.w_len = (size_t)L.m_tiles * L.n_chunks * slab_bf16 / 2;  // in floats
       off += (L.w_len + 63) & ~(size_t)63;
@@ -297,7 +297,7 @@ inline float bf2f(uint16_t b) {
 //   tap = tg*TPC + jj; plane 0 = bf16(w), plane 1 = bf16(w - hi).
 void pack_bf16x3(const Layer& L, const float* w, uint16_t* dst) {
   const hfg::Bf16x3Cfg& t = hfg::kBf16x3Tiles[L.tile];
-  const int TPC = hfg::kBf16x3Tpc;
+  const int TPC = t.TPC;
   const int n_g = (L.C_in + 15) / 16, n_tg = (L.KT + TPC - 1) / TPC;
   size_t idx = 0;
   for (int mt = 0; mt < L.m_tiles; ++mt)

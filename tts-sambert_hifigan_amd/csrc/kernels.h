@@ -84,18 +84,22 @@ constexpr int kMaxDil = 16;
 constexpr int halo_max(int dkt) { return dkt == 0 ? 192 : (dkt - 1) * kMaxDil; }
 
 // ---- split-precision bf16x3 conv (conv_bf16x3.hip) ----
-// 8-wave tiles: B0 = 128 x 256 (2x4 waves of 64x64), B1 = 64 x 256 (1x8 waves of 64x32).
+// B0 = 128 x 256 (2x4 waves of 64x64, 4 taps per chunk, 1 block per CU),
+// B1 = 64 x 256 (1x4 waves of 64x64, 2 taps per chunk, 2 blocks per CU),
+// B2 = 32 x 256 (1x4 waves of 32x64, 4 taps per chunk, 2 blocks per CU).
 struct Bf16x3Cfg {
-  int WAVES_M, WAVES_N, WM, WN;
+  int WAVES_M, WAVES_N, WM, WN, TPC;
   constexpr int MT() const { return 32 * WM * WAVES_M; }
   constexpr int NTILE() const { return 32 * WN * WAVES_N; }
   constexpr int threads() const { return 64 * WAVES_M * WAVES_N; }
 };
-constexpr int kBf16x3Tiles_n = 2;
-constexpr Bf16x3Cfg kBf16x3Tiles[kBf16x3Tiles_n] = {{2, 4, 2, 2}, {1, 8, 2, 1}};
-constexpr int kBf16x3Tpc = 4;  // taps per chunk (chunk = 16 channels x 4 taps)
+constexpr int kBf16x3Tiles_n = 3;
+constexpr Bf16x3Cfg kBf16x3Tiles[kBf16x3Tiles_n] = {
+    {2, 4, 2, 2, 4}, {1, 4, 2, 2, 2}, {1, 4, 1, 2, 4}};
 constexpr int kBf16x3Ck = 16;  // channels per chunk (one MFMA k-step per tap)
-inline int bf16x3_tile_for_rows(int M) { return M >= 128 ? 0 : (M >= 64 ? 1 : -1); }
+inline int bf16x3_tile_for_rows(int M) {
+  return M >= 128 ? 0 : (M >= 64 ? 1 : (M >= 32 ? 2 : -1));
+}
 size_t bf16x3_lds_bytes(int tile, int kt, int dil);
 hipError_t launch_conv_bf16x3(int tile, int kt, const ConvParams& p, int n_tiles, int m_tiles,
                               int batch, hipStream_t stream, const char** name);
