@@ -200,6 +200,10 @@ conv1d_mfma_f32(const ConvParams p) {
   if constexpr (UPS) {
 #pragma unroll
     for (int i = 0; i < WM; ++i) {
+      float bv[16];  // batch the bias loads ahead of the scattered stores
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        bv[r] = p.bias[mt * MT + wave_m * 32 * WM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * half];
 #pragma unroll
       for (int k = 0; k < WN; ++k) {
         const int n = n0 + wave_n * 32 * WN + k * 32 + col;
@@ -208,7 +212,7 @@ conv1d_mfma_f32(const ConvParams p) {
         for (int r = 0; r < 16; ++r) {
           const int row = mt * MT + wave_m * 32 * WM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
           if (row >= p.M) continue;
-          const float v = acc[i][k][r] + p.bias[row];
+          const float v = acc[i][k][r] + bv[r];
           const int co = row / p.ups_s;
           const int ph = row - co * p.ups_s;
           const int t = n * p.ups_s + ph - p.ups_p;

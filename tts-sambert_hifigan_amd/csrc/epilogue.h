@@ -2,8 +2,11 @@
 // (regular Conv1d, not the polyphase upsampler):
 //   v = acc + bias[row]; v = res + v (ResBlock residual, models/hifigan.py:85);
 //   v = lrelu(v) (post-activation, :83); MRF running sum / final division (:125-131)
-// Addresses are 32-bit byte offsets from block-uniform batch bases so every
-// load/store is an SGPR-base + VGPR-offset access (no per-element 64-bit math).
+// Per 32x32 accumulator tile the 16 bias, 16 residual and 16 MRF loads are issued
+// as independent batches (unconditional, clamped offsets) before any store, so a
+// tile costs one memory round trip instead of one per element (the residual may
+// alias the output: every element is still read before its own write).
+// Addresses are 32-bit byte offsets from block-uniform batch bases.
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -19,29 +22,57 @@ __device__ __forceinline__ void conv_epilogue(const ConvParams& p, floatx16e (&a
                                               int b, int row_base, int n_base, int N_b,
                                               int half, int col) {
   const int64_t bo = (int64_t)b * p.y_bs;
-  const char* __restrict__ resb = p.res ? reinterpret_cast<const char*>(p.res + bo) : nullptr;
-  char* __restrict__ outb = reinterpret_cast<char*>((p.mrf ? p.mrf : p.y) + bo);
+  const char* resb = p.res ? reinterpret_cast<const char*>(p.res + bo) : nullptr;
+  char* outb = reinterpret_cast<char*>((p.mrf ? p.mrf : p.y) + bo);
   const bool add_mrf = p.mrf && (p.mrf_mode & 1);
   const bool div_mrf = p.mrf && (p.mrf_mode & 2);
   const bool act = p.act_out != 0;
+  const float* __restrict__ bias = p.bias;  // padded to the m-tile: every row index is readable
 #pragma unroll
   for (int i = 0; i < WM; ++i) {
+    float bv[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r)
+      bv[r] = bias[row_base + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * half];
 #pragma unroll
     for (int k = 0; k < WN; ++k) {
       const int n = n_base + k * 32 + col;
-      if (n >= N_b) continue;
+      const bool nok = n < N_b;
+      unsigned off[16];
+      bool ok[16];
+      float v[16];
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int row = row_base + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
-        if (row >= p.M) continue;
-        const unsigned off = (unsigned)(row * p.N + n) * 4u;
-        float v = acc[i][k][r] + p.bias[row];
-        if (resb) v = *reinterpret_cast<const float*>(resb + off) + v;
-        if (act) v = v > 0.f ? v : v * kLReluSlope;
-        if (add_mrf) v = *reinterpret_cast<const float*>(outb + off) + v;
-        if (div_mrf) v = v / p.mrf_div;
-        *reinterpret_cast<float*>(outb + off) = v;
+        ok[r] = nok && row < p.M;
+        off[r] = ok[r] ? (unsigned)(row * p.N + n) * 4u : 0u;
+        v[r] = acc[i][k][r] + bv[r];
       }
+      if (resb) {
+        float rv[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) rv[r] = *reinterpret_cast<const float*>(resb + off[r]);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) v[r] = rv[r] + v[r];
+      }
+      if (act) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) v[r] = v[r] > 0.f ? v[r] : v[r] * kLReluSlope;
+      }
+      if (add_mrf) {
+        float mv[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) mv[r] = *reinterpret_cast<const float*>(outb + off[r]);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) v[r] = mv[r] + v[r];
+      }
+      if (div_mrf) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) v[r] = v[r] / p.mrf_div;
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        if (ok[r]) *reinterpret_cast<float*>(outb + off[r]) = v[r];
     }
   }
 }
