@@ -1,5 +1,9 @@
+# rocprofv3 kernel-trace stats + separate FETCH_SIZE / WRITE_SIZE passes of bench.py
+# (PMC passes carry no trace domains: MI355X_MICROARCH.md §HBM / gpurun rules).
+# usage on the GPU box:  bash profiles/run_rocprof.sh <tag>
 cd /tmp && export TMPDIR=/tmp
 R=$GRAFT_REPO_ROOT
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof_v2 -o run --output-format csv -- python $R/bench.py --steps 5 --warmup 2 --no-cpu-baseline > $R/gpurun_out/prof_v2_bench.json 2> $R/gpurun_out/prof_v2_bench.err && \
-timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d $R/gpurun_out/pmc_fetch -o run --output-format csv -- python $R/bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-profile > $R/gpurun_out/pmc_fetch.log 2>&1 && \
-timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d $R/gpurun_out/pmc_write -o run --output-format csv -- python $R/bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-profile > $R/gpurun_out/pmc_write.log 2>&1
+T=${1:-cur}
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof_$T -o run --output-format csv -- python $R/bench.py --steps 5 --warmup 2 --also --no-cpu-baseline > $R/gpurun_out/prof_${T}_bench.json 2> $R/gpurun_out/prof_${T}_bench.err && \
+timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d $R/gpurun_out/pmc_fetch_$T -o run --output-format csv -- python $R/bench.py --steps 2 --warmup 1 --also --no-cpu-baseline --no-profile > $R/gpurun_out/pmc_fetch_$T.log 2>&1 && \
+timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d $R/gpurun_out/pmc_write_$T -o run --output-format csv -- python $R/bench.py --steps 2 --warmup 1 --also --no-cpu-baseline --no-profile > $R/gpurun_out/pmc_write_$T.log 2>&1

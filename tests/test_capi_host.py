@@ -253,3 +253,58 @@ def test_bf16x3_packing(pkg, preset):
         assert err < 2.0 ** -15, (mod, err)
         assert np.array_equal(bias[:cout], sd[mod + ".bias"])
     assert n_checked >= 2
+
+
+def unpack_bf16x3(info, packed, waves):
+    """Invert conv_bf16x3's fragment order → Wt[row][ci][tap] (hi + lo, float64)."""
+    wm_, WM, TPC = waves
+    MT = info["MT"]
+    n_chunks, KT = info["n_chunks"], info["KT"]
+    n_tg = -(-KT // TPC)
+    n_g = n_chunks // n_tg
+    u = packed.view(np.uint16).reshape(info["m_tiles"], n_g, n_tg, TPC, 2, wm_, WM, 64, 8)
+    val = bf2f(u[:, :, :, :, 0]).astype(np.float64) + bf2f(u[:, :, :, :, 1])
+    Wt = np.zeros((info["m_tiles"] * MT, n_g * 16, n_tg * TPC))
+    lane = np.arange(64)
+    for mt in range(info["m_tiles"]):
+        for g in range(n_g):
+            for tg in range(n_tg):
+                for jj in range(TPC):
+                    for wv in range(wm_):
+                        for wm in range(WM):
+                            rows = mt * MT + wv * 32 * WM + wm * 32 + (lane & 31)
+                            for e in range(8):
+                                Wt[rows, g * 16 + 8 * (lane >> 5) + e, tg * TPC + jj] = \
+                                    val[mt, g, tg, jj, wv, wm, :, e]
+    return Wt[: info["M"], :, :KT]
+
+
+def test_bf16x3_polyphase_upsampler_packing(pkg):
+    cfg = C.NONEXACT  # odd k-u on the first stages
+    sd = C.make_state_dict(cfg, seed=41)
+    h = host_handle(pkg, cfg, "bf16x3")
+    for k, v in sd.items():
+        h.set_weight(k, torch.from_numpy(v))
+    h.commit()
+    waves = {0: (2, 2, 4), 1: (1, 2, 2), 2: (1, 1, 4)}
+    rng = np.random.default_rng(1)
+    c0 = cfg.upsample_initial_channel
+    for i, (u, k) in enumerate(zip(cfg.upsample_rates, cfg.upsample_kernel_sizes)):
+        info, packed, bias = h.packed_layer(f"ups.{i}")
+        cin, cout = c0 >> i, c0 >> (i + 1)
+        assert info["kind"] == 1 and info["CK"] == 16
+        Wt = unpack_bf16x3(info, packed, waves[info["tile"]])[:, :cin]
+        x = rng.standard_normal((cin, 9)).astype(np.float32)
+        ref = F.conv_transpose1d(torch.from_numpy(x)[None], torch.from_numpy(sd[f"ups.{i}.weight"]),
+                                 torch.from_numpy(sd[f"ups.{i}.bias"]), u, (k - u) // 2)[0].numpy()
+        Lout, p = ref.shape[-1], (k - u) // 2
+        N = (Lout - 1 + p) // u + 1
+        g = emulate_conv(Wt, bias, x, -(info["KT"] - 1), 1, N)
+        y = np.full((cout, Lout), np.nan)
+        for m in range(cout * u):
+            co, r = divmod(m, u)
+            t = np.arange(N) * u + r - p
+            ok = (t >= 0) & (t < Lout)
+            y[co, t[ok]] = g[m, ok]
+        assert not np.isnan(y).any()
+        assert np.abs(y - ref).max() < 1e-3 * np.abs(ref).max()

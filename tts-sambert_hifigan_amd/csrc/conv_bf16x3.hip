@@ -34,7 +34,7 @@ typedef __attribute__((address_space(1))) void* gptr_t1;
 
 __device__ __forceinline__ float lrelu3(float v) { return v > 0.f ? v : v * kLReluSlope; }
 
-template <int KT_, int TPC, int WAVES_M, int WAVES_N, int WM, int WN>
+template <int KT_, int TPC, int WAVES_M, int WAVES_N, int WM, int WN, bool UPS>
 __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N, 2)
 conv1d_bf16x3(const ConvParams p) {
   constexpr int NW = WAVES_M * WAVES_N;
@@ -72,8 +72,13 @@ conv1d_bf16x3(const ConvParams p) {
   const __bf16* __restrict__ wsrc =
       reinterpret_cast<const __bf16*>(p.w) + (int64_t)mt * p.n_chunks * SLAB;
   const int L_in_b = p.len_in ? p.len_in[b] : p.L_in;
-  const int N_b = p.len_out ? p.len_out[b] : p.N;
+  int N_b = p.N;
+  if (p.len_out) {
+    const int lo = p.len_out[b];
+    N_b = UPS ? (lo > 0 ? (lo - 1 + p.ups_p) / p.ups_s + 1 : 0) : lo;
+  }
   if (n0 >= N_b) return;  // whole tile past this utterance's end (block-uniform)
+  const int L_out_b = (UPS && p.len_out) ? p.len_out[b] : p.L_out;
   const int xcs = (int)p.x_cs, xts = (int)p.x_ts;
   const int wbase = n0 + p.off;                   // input index of window row 0
 
@@ -215,37 +220,63 @@ conv1d_bf16x3(const ConvParams p) {
   }
 
   // ---- epilogue (same contract as conv1d_mfma_f32) ----
-  conv_epilogue<WM, WN>(p, acc, b, mt * MT + wave_m * 32 * WM, n0 + wave_n * 32 * WN, N_b, half,
-                        col);
+  if constexpr (UPS) {
+    // polyphase scatter: GEMM row m = co*s + r lands at t = n*s + r - p
+#pragma unroll
+    for (int i = 0; i < WM; ++i) {
+      float bv[16];
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        bv[r] = p.bias[mt * MT + wave_m * 32 * WM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * half];
+#pragma unroll
+      for (int k = 0; k < WN; ++k) {
+        const int n = n0 + wave_n * 32 * WN + k * 32 + col;
+        if (n >= N_b) continue;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int row = mt * MT + wave_m * 32 * WM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
+          if (row >= p.M) continue;
+          const int co = row / p.ups_s;
+          const int t = n * p.ups_s + (row - co * p.ups_s) - p.ups_p;
+          if (t >= 0 && t < L_out_b)
+            p.y[(int64_t)b * p.y_bs + (int64_t)co * p.L_out + t] = acc[i][k][r] + bv[r];
+        }
+      }
+    }
+  } else {
+    conv_epilogue<WM, WN>(p, acc, b, mt * MT + wave_m * 32 * WM, n0 + wave_n * 32 * WN, N_b,
+                          half, col);
+  }
 }
 
 namespace {
 
 typedef void (*ConvFn3)(const ConvParams);
 
-template <int KT, int TILE>
+template <int KT, int TILE, bool UPS>
 struct Inst3 {
   static constexpr Bf16x3Cfg t = kBf16x3Tiles[TILE];
   static ConvFn3 fn() {
-    return conv1d_bf16x3<KT, t.TPC, t.WAVES_M, t.WAVES_N, t.WM, t.WN>;
+    return conv1d_bf16x3<KT, t.TPC, t.WAVES_M, t.WAVES_N, t.WM, t.WN, UPS>;
   }
 };
 
 struct Entry3 {
   int kt;
   int tile;
+  bool ups;
   ConvFn3 fn;
   bool attr;
   char name[96];
 };
 
-#define HFG3_ENTRY(KT, TILE) \
-  { KT, TILE, Inst3<KT, TILE>::fn(), false, {0} }
+#define HFG3_ENTRY(KT, TILE, UPS) \
+  { KT, TILE, UPS, Inst3<KT, TILE, UPS>::fn(), false, {0} }
+#define HFG3_TILES(KT, UPS) HFG3_ENTRY(KT, 0, UPS), HFG3_ENTRY(KT, 1, UPS), HFG3_ENTRY(KT, 2, UPS)
 
 Entry3 g_entries3[] = {
-    HFG3_ENTRY(3, 0), HFG3_ENTRY(5, 0), HFG3_ENTRY(7, 0), HFG3_ENTRY(11, 0), HFG3_ENTRY(0, 0),
-    HFG3_ENTRY(3, 1), HFG3_ENTRY(5, 1), HFG3_ENTRY(7, 1), HFG3_ENTRY(11, 1), HFG3_ENTRY(0, 1),
-    HFG3_ENTRY(3, 2), HFG3_ENTRY(5, 2), HFG3_ENTRY(7, 2), HFG3_ENTRY(11, 2), HFG3_ENTRY(0, 2),
+    HFG3_TILES(3, false), HFG3_TILES(5, false), HFG3_TILES(7, false), HFG3_TILES(11, false),
+    HFG3_TILES(0, false), HFG3_TILES(2, true),  HFG3_TILES(0, true),
 };
 
 }  // namespace
@@ -258,12 +289,12 @@ size_t bf16x3_lds_bytes(int tile, int kt, int dil) {
   return sizeof(__bf16) * (2 * slab + 2 * 2 * xplane);  // 2 weight slabs + 2 (hi,lo) windows
 }
 
-hipError_t launch_conv_bf16x3(int tile, int kt, const ConvParams& p, int n_tiles, int m_tiles,
-                              int batch, hipStream_t stream, const char** name) {
+hipError_t launch_conv_bf16x3(int tile, int kt, bool ups, const ConvParams& p, int n_tiles,
+                              int m_tiles, int batch, hipStream_t stream, const char** name) {
   Entry3* e = nullptr;
   Entry3* generic = nullptr;
   for (auto& cand : g_entries3) {
-    if (cand.tile != tile) continue;
+    if (cand.tile != tile || cand.ups != ups) continue;
     if (cand.kt == kt) e = &cand;
     if (cand.kt == 0) generic = &cand;
   }
@@ -272,8 +303,8 @@ hipError_t launch_conv_bf16x3(int tile, int kt, const ConvParams& p, int n_tiles
   if (p.dil > kMaxDil || (e->kt == 0 && kt > 16)) return hipErrorInvalidValue;
   const Bf16x3Cfg& t = kBf16x3Tiles[tile];
   if (!e->name[0])
-    snprintf(e->name, sizeof(e->name), "conv1d_bf16x3<%d, %d, %d, %d, %d, %d>", e->kt, t.TPC,
-             t.WAVES_M, t.WAVES_N, t.WM, t.WN);
+    snprintf(e->name, sizeof(e->name), "conv1d_bf16x3<%d, %d, %d, %d, %d, %d, %s>", e->kt, t.TPC,
+             t.WAVES_M, t.WAVES_N, t.WM, t.WN, e->ups ? "true" : "false");
   const size_t lds = bf16x3_lds_bytes(tile, kt, p.dil);
   if (lds > 160 * 1024) return hipErrorInvalidValue;
   if (!e->attr) {

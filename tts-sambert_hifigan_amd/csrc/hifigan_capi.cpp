@@ -219,7 +219,7 @@ void build_layers(hfg_handle* h) {
       off += 64;
       continue;
     }
-    if (h->cfg.dtype == HFG_DTYPE_BF16X3 && L.kind == L_CONV &&
+    if (h->cfg.dtype == HFG_DTYPE_BF16X3 && (L.kind == L_CONV || L.kind == L_UPS) &&
         hfg::bf16x3_tile_for_rows(L.M) >= 0) {
       // split-precision path: chunk = 16 channels x TPC taps
       const hfg::Bf16x3Cfg& t3 = hfg::kBf16x3Tiles[hfg::bf16x3_tile_for_rows(L.M)];
@@ -295,7 +295,8 @@ inline float bf2f(uint16_t b) {
 //         + lane*8 + e
 //   row = mt*MT + wave_m*32*WM + wm*32 + (lane & 31), ci = g*16 + 8*(lane >> 5) + e,
 //   tap = tg*TPC + jj; plane 0 = bf16(w), plane 1 = bf16(w - hi).
-void pack_bf16x3(const Layer& L, const float* w, uint16_t* dst) {
+template <typename F>
+void pack_bf16x3(const Layer& L, F wt, uint16_t* dst) {
   const hfg::Bf16x3Cfg& t = hfg::kBf16x3Tiles[L.tile];
   const int TPC = t.TPC;
   const int n_g = (L.C_in + 15) / 16, n_tg = (L.KT + TPC - 1) / TPC;
@@ -313,8 +314,7 @@ void pack_bf16x3(const Layer& L, const float* w, uint16_t* dst) {
                     const int ci = g * 16 + 8 * (lane >> 5) + e;
                     const int tap = tg * TPC + jj;
                     float v = 0.f;
-                    if (row < L.M && ci < L.C_in && tap < L.KT)
-                      v = w[((size_t)row * L.C_in + ci) * L.k + tap];
+                    if (row < L.M && ci < L.C_in && tap < L.KT) v = wt(row, ci, tap);
                     const uint16_t hi = f2bf(v);
                     dst[idx++] = plane == 0 ? hi : f2bf(v - bf2f(hi));
                   }
@@ -332,8 +332,22 @@ void pack_layer(hfg_handle* h, const Layer& L) {
     return;
   }
   if (L.kind == L_CONV && L.prec == 1) {
-    pack_bf16x3(L, w, reinterpret_cast<uint16_t*>(dst));
+    const int cin = L.C_in, k = L.k;
+    pack_bf16x3(L, [&](int row, int ci, int j) { return w[((size_t)row * cin + ci) * k + j]; },
+                reinterpret_cast<uint16_t*>(dst));
     for (size_t m = 0; m < L.b_len; ++m) bdst[m] = m < (size_t)L.M ? Bp.data[m] : 0.f;
+    return;
+  }
+  if (L.kind == L_UPS && L.prec == 1) {
+    const int s = L.s, Q = L.KT, k = L.k, cout = L.C_out;
+    pack_bf16x3(L,
+                [&](int row, int ci, int jj) {
+                  const int co = row / s, r = row % s;
+                  const int kidx = r + s * (Q - 1 - jj);
+                  return kidx < k ? w[((size_t)ci * cout + co) * k + kidx] : 0.f;
+                },
+                reinterpret_cast<uint16_t*>(dst));
+    for (size_t m = 0; m < L.b_len; ++m) bdst[m] = m < (size_t)L.M ? Bp.data[m / s] : 0.f;
     return;
   }
   if (L.kind == L_CONV) {
@@ -493,7 +507,7 @@ int run_conv(hfg_handle* h, Launcher& ln, const Layer& L, const float* x, int64_
   const char* name = nullptr;
   ln.begin(flop, bytes);
   hipError_t e = L.prec == 1
-                     ? hfg::launch_conv_bf16x3(L.tile, L.KT, p, n_tiles, L.m_tiles, (int)B,
+                     ? hfg::launch_conv_bf16x3(L.tile, L.KT, false, p, n_tiles, L.m_tiles, (int)B,
                                                ln.stream, &name)
                      : hfg::launch_conv((TileId)L.tile, L.KT, false, p, n_tiles, L.m_tiles,
                                         (int)B, ln.stream, &name);
@@ -504,7 +518,6 @@ int run_conv(hfg_handle* h, Launcher& ln, const Layer& L, const float* x, int64_
 
 int run_ups(hfg_handle* h, Launcher& ln, const Layer& L, const float* x, int64_t B, int64_t Lin,
             int64_t Lout, float* y, const int32_t* len_in, const int32_t* len_out) {
-  const TileCfg& t = kTiles[L.tile];
   ConvParams p{};
   p.x = x;
   p.x_bs = (int64_t)L.C_in * Lin;
@@ -530,13 +543,18 @@ int run_ups(hfg_handle* h, Launcher& ln, const Layer& L, const float* x, int64_t
   p.ups_p = L.p;
   p.L_out = (int)Lout;
   p.n_chunks = L.n_chunks;
-  const int n_tiles = (p.N + t.NTILE() - 1) / t.NTILE();
+  p.dbg = h->dbg_flags;
+  const int ntile = L.prec == 1 ? hfg::kBf16x3Tiles[L.tile].NTILE() : kTiles[L.tile].NTILE();
+  const int n_tiles = (p.N + ntile - 1) / ntile;
   const double flop = 2.0 * L.C_in * L.C_out * L.k * (double)Lin * B;
   const double bytes = 4.0 * B * (L.C_in * Lin + L.C_out * Lout) + 4.0 * L.C_in * L.C_out * L.k;
   const char* name = nullptr;
   ln.begin(flop, bytes);
-  hipError_t e = hfg::launch_conv((TileId)L.tile, L.KT, true, p, n_tiles, L.m_tiles, (int)B,
-                                  ln.stream, &name);
+  hipError_t e = L.prec == 1
+                     ? hfg::launch_conv_bf16x3(L.tile, L.KT, true, p, n_tiles, L.m_tiles, (int)B,
+                                               ln.stream, &name)
+                     : hfg::launch_conv((TileId)L.tile, L.KT, true, p, n_tiles, L.m_tiles, (int)B,
+                                        ln.stream, &name);
   ln.end(name);
   if (e != hipSuccess) return fail(HFG_EIO, "launch %s: %s", L.mod.c_str(), hipGetErrorString(e));
   return HFG_OK;

@@ -101,8 +101,8 @@ inline int bf16x3_tile_for_rows(int M) {
   return M >= 128 ? 0 : (M >= 64 ? 1 : (M >= 32 ? 2 : -1));
 }
 size_t bf16x3_lds_bytes(int tile, int kt, int dil);
-hipError_t launch_conv_bf16x3(int tile, int kt, const ConvParams& p, int n_tiles, int m_tiles,
-                              int batch, hipStream_t stream, const char** name);
+hipError_t launch_conv_bf16x3(int tile, int kt, bool ups, const ConvParams& p, int n_tiles,
+                              int m_tiles, int batch, hipStream_t stream, const char** name);
 
 // Launch the conv kernel for (tile, taps, ups).  Returns a hipError_t and,
 // via *name, the kernel's template-instance name (as rocprofv3 prints it).
