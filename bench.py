@@ -64,6 +64,8 @@ def parse():
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl = RCCL over xGMI (production); gloo only to rehearse N>1 on one GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-extra", action="store_true",
+                    help="skip the other BASELINE configs (C1 latency + hipGraph, C4 V2*, C5 ragged)")
     ap.add_argument("--cpu-budget-s", type=float, default=12.0)
     ap.add_argument("--no-profile", action="store_true",
                     help="do not bracket launches with HIP events (no roofline)")
@@ -92,6 +94,75 @@ def cpu_baseline(cfg, sd, frames, budget_s):
                       f"after warm-up, oracle/hifigan_torch.py (same ATen ops as the reference), "
                       f"{threads} threads, {os.cpu_count()} host CPUs visible",
             "rtf": best / (samples / SAMPLE_RATE)}
+
+
+def extra_configs(pkg, C, dev, precision, steps=5):
+    """The other BASELINE.json configs, measured on this GPU (rank 0, N=1):
+    C1 V1 [1,80,256] latency, eager vs a captured hipGraph replay (torch.cuda.graph
+    around the same forward: 78 launches on the capture stream); C4 pinned V2*
+    [16,80,2048]; C5 the acoustic->vocoder glue on 32 ragged utterances of 60-63
+    frames in the acoustic model's [B,T,80] layout."""
+    import importlib
+    glue = importlib.import_module(ge.PKG_NAME + ".glue")
+    out = {}
+
+    def timed(fn, n):
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for _ in range(n):
+            fn()
+        torch.cuda.synchronize(dev)
+        return (time.perf_counter() - t0) / n
+
+    def make(cfg):
+        gen = pkg.HiFiGANGenerator(**cfg.kwargs(), precision=precision).eval()
+        gen.load_state_dict({k: torch.from_numpy(v) for k, v in C.make_state_dict(cfg, 0).items()})
+        return gen.to(dev)
+
+    g = torch.Generator().manual_seed(1234)
+    with torch.no_grad():
+        gen = make(C.V1)
+        mel = torch.randn(1, 80, 256, generator=g).to(dev)
+        for _ in range(3):
+            gen(mel)
+        eager = timed(lambda: gen(mel), 20)
+        s = torch.cuda.Stream(dev)
+        s.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(s):
+            for _ in range(2):
+                gen(mel)
+        torch.cuda.current_stream(dev).wait_stream(s)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            wav_g = gen(mel)
+        graph.replay()
+        replay = timed(graph.replay, 20)
+        ok = bool(torch.equal(wav_g, gen(mel)))
+        out["C1_v1_1x80x256"] = {"eager_ms": eager * 1e3, "hipgraph_ms": replay * 1e3,
+                                 "samples_per_s_hipgraph": 65536 / replay,
+                                 "rtf_hipgraph": replay / (65536 / SAMPLE_RATE),
+                                 "graph_equals_eager": ok}
+        del gen
+        gen = make(C.V2STAR)
+        mel = torch.randn(16, 80, 2048, generator=g).to(dev)
+        for _ in range(2):
+            gen(mel)
+        t = timed(lambda: gen(mel), steps)
+        out["C4_v2star_16x80x2048"] = {"ms_per_step": t * 1e3, "samples_per_s": 16 * 2048 * 256 / t,
+                                       "rtf": t / (16 * 2048 * 256 / SAMPLE_RATE)}
+        del gen
+        gen = make(C.V1)
+        lens = [int(x) for x in torch.randint(60, 64, (32,), generator=g)]
+        mel_pred = torch.randn(32, max(lens), 80, generator=g).to(dev)
+        for _ in range(2):
+            glue.vocode_acoustic(gen, mel_pred, lens)
+        t = timed(lambda: glue.vocode_acoustic(gen, mel_pred, lens), steps)
+        valid = sum(lens) * 256
+        out["C5_glue_32_ragged_60to63"] = {"ms_per_step": t * 1e3, "samples_per_s": valid / t,
+                                           "frames": lens[:8] + ["..."],
+                                           "note": "vocoder half of config 5; the SAM-BERT "
+                                                   "acoustic model is CPU reference code (out of scope)"}
+    return out
 
 
 def main():
@@ -292,6 +363,8 @@ def main():
                                "ms_per_step": v["ms"] / args.steps,
                                "TFLOPs": v["flop"] / (v["ms"] * 1e-3) / 1e12 if v["ms"] else None}
                            for k, v in sorted(prof.items(), key=lambda kv: -kv[1]["ms"])}
+    if world == 1 and not args.no_extra:
+        line["extra_configs"] = extra_configs(pkg, C, dev, args.precision)
     if world == 1 and not args.no_cpu_baseline:
         cfg_np = C.make_state_dict(cfg, seed=0) if sd_np is None else sd_np
         line["cpu_baseline"] = cpu_baseline(cfg, cfg_np, T, args.cpu_budget_s)

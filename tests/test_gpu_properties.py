@@ -185,3 +185,26 @@ def test_profiling_summary(pkg, v1, dev):
     from oracle import config as C
     total_flop = sum(v["flop"] for v in prof.values())
     assert abs(total_flop - 2398848 * 64 * 256) / total_flop < 1e-5  # summary prints 7 digits
+
+
+def test_hipgraph_capture_replay(v1, dev):
+    """The 78 launches of one forward can be captured into a hipGraph (torch.cuda.graph
+    on the capture stream) and replayed; the replay equals the eager result."""
+    gen, _ = v1
+    mel = torch.randn(2, 80, 40, device=dev)
+    with torch.no_grad():
+        ref = gen(mel)
+        s = torch.cuda.Stream(dev)
+        s.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(s):
+            gen(mel)
+        torch.cuda.current_stream(dev).wait_stream(s)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            out = gen(mel)
+        mel.copy_(torch.randn(2, 80, 40, device=dev))
+        g.replay()
+        ref2 = gen(mel)
+    torch.cuda.synchronize()
+    assert torch.equal(out, ref2)
+    assert not torch.equal(out, ref)
