@@ -47,6 +47,7 @@ conv1d_bf16x3(const ConvParams p) {
   constexpr int KT_MAX = KT_ > 0 ? KT_ : 16;
   constexpr int XW_MAX = NTILE + (KT_MAX - 1) * kMaxDil;
   constexpr int XQ = (2 * XW_MAX + NT - 1) / NT;  // staging tasks per thread
+  static_assert(XQ * 8 <= 32, "ok mask");
   const int KT = KT_ > 0 ? KT_ : p.kt;
   const int n_tg = (KT + TPC - 1) / TPC;          // tap groups per channel group
   // one staged input window per 16-channel group serves all KT taps
@@ -99,9 +100,13 @@ conv1d_bf16x3(const ConvParams p) {
     }
   };
   // ---- activations: task = (window row t, 8 channels), 32-bit offsets from xb ----
+  // raw loads (clamped offsets) into registers; the zero padding is applied at store
+  // time from a bit mask, so the loads' latency hides behind the chunk's MFMAs
   float xv[XQ][8];
+  uint32_t xok = 0;
   auto load_x = [&](int g) {
     const bool full = g * 16 + 16 <= p.C_in;  // block-uniform
+    xok = 0;
 #pragma unroll
     for (int q = 0; q < XQ; ++q) {
       const int i = tid + q * NT;
@@ -112,11 +117,14 @@ conv1d_bf16x3(const ConvParams p) {
       // byte offsets from the block-uniform base: SGPR base + 32-bit VGPR offset loads
       const unsigned o0 = tok ? (unsigned)(cb * xcs + gi * xts) * 4u : 0u;
       const unsigned step = tok ? (unsigned)xcs * 4u : 0u;
+      // channels past C_in (a partial last group) re-read the last valid channel
+      const int ecap = full ? 7 : min(p.C_in - 1 - cb, 7);
+      const uint32_t m8 = tok ? (ecap >= 7 ? 0xffu : (ecap < 0 ? 0u : (1u << (ecap + 1)) - 1u)) : 0u;
+      xok |= m8 << (q * 8);
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
-        const bool ok = tok && (full || cb + e < p.C_in);
-        const float v = *reinterpret_cast<const float*>(reinterpret_cast<const char*>(xb) + (o0 + e * step));
-        xv[q][e] = ok ? v : 0.f;
+        const unsigned oe = o0 + (unsigned)(full ? e : max(min(e, ecap), 0)) * step;
+        xv[q][e] = *reinterpret_cast<const float*>(reinterpret_cast<const char*>(xb) + oe);
       }
     }
   };
@@ -129,7 +137,7 @@ conv1d_bf16x3(const ConvParams p) {
         bf16x8 h, l;
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
-          float v = xv[q][e];
+          float v = (xok >> (q * 8 + e)) & 1u ? xv[q][e] : 0.f;
           if (p.act_in) v = lrelu3(v);
           const __bf16 hh = (__bf16)v;
           h[e] = hh;
