@@ -206,17 +206,19 @@ def bf2f(u16):
     return (u16.astype(np.uint32) << 16).view(np.float32)
 
 
+@pytest.mark.parametrize("big_tile", ["0", "3"])
 @pytest.mark.parametrize("preset", ["v1", "v2star"])
-def test_bf16x3_packing(pkg, preset):
+def test_bf16x3_packing(pkg, preset, big_tile, monkeypatch):
     """bf16x3 layers: the packed hi/lo planes reconstruct every weight to ~2^-16
-    relative, in the fragment order of conv_bf16x3.hip."""
+    relative, in the fragment order of conv_bf16x3.hip (both tiles for M >= 128)."""
+    monkeypatch.setenv("HFG_BF16X3_BIGTILE", big_tile)
     cfg = C.PRESETS[preset]
     sd = C.make_state_dict(cfg, seed=31)
     h = host_handle(pkg, cfg, "bf16x3")
     for k, v in sd.items():
         h.set_weight(k, torch.from_numpy(v))
     h.commit()
-    WAVES = {0: (2, 2, 4), 1: (1, 2, 2), 2: (1, 1, 4)}  # tile -> (WAVES_M, WM, TPC)
+    WAVES = {0: (2, 2, 4), 1: (1, 2, 2), 2: (1, 1, 4), 3: (2, 2, 2)}  # tile -> (WAVES_M, WM, TPC)
     n_checked = 0
     for mod in ["conv_pre", "mrfs.0.resblocks.2.convs1.1", "mrfs.1.resblocks.0.convs2.1",
                 "mrfs.2.resblocks.1.convs1.0", "mrfs.3.resblocks.2.convs2.1"]:

@@ -34,7 +34,21 @@ typedef __attribute__((address_space(1))) void* gptr_t1;
 
 __device__ __forceinline__ float lrelu3(float v) { return v > 0.f ? v : v * kLReluSlope; }
 
-template <int KT_, int TPC, int WAVES_M, int WAVES_N, int WM, int WN, bool UPS>
+// s_waitcnt vmcnt(N) with a compile-time N
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+// workgroup barrier over LDS writes made by ds_write (lgkmcnt): the caller has already
+// waited (vmcnt) for the LDS-DMA pieces the next chunk reads.  Written as one asm block
+// so no fence makes the compiler wait for every outstanding global load / LDS-DMA
+// piece, and the "memory" clobber keeps LDS accesses on their side of the barrier.
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+template <int KT_, int TPC, int WAVES_M, int WAVES_N, int WM, int WN, int WD, bool UPS>
 __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N, 2)
 conv1d_bf16x3(const ConvParams p) {
   constexpr int NW = WAVES_M * WAVES_N;
@@ -48,6 +62,10 @@ conv1d_bf16x3(const ConvParams p) {
   constexpr int XW_MAX = NTILE + (KT_MAX - 1) * kMaxDil;
   constexpr int XQ = (2 * XW_MAX + NT - 1) / NT;  // staging tasks per thread
   static_assert(XQ * 8 <= 32, "ok mask");
+  constexpr int NX = XQ * 8;                      // input loads per thread per channel group
+  constexpr int PW = SLAB / 8 / 64 / NW;          // LDS-DMA pieces per thread per slab
+  static_assert(PW * 8 * 64 * NW == SLAB, "slab must split evenly over the waves");
+  static_assert(NX + PW < 64, "vmcnt range");
   const int KT = KT_ > 0 ? KT_ : p.kt;
   const int n_tg = (KT + TPC - 1) / TPC;          // tap groups per channel group
   // one staged input window per 16-channel group serves all KT taps
@@ -57,7 +75,7 @@ conv1d_bf16x3(const ConvParams p) {
 
   extern __shared__ __attribute__((aligned(16))) __bf16 lds16[];
   __bf16* const Wbuf0 = lds16;
-  __bf16* const Xbuf0 = lds16 + 2 * SLAB;
+  __bf16* const Xbuf0 = lds16 + WD * SLAB;
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -88,18 +106,17 @@ conv1d_bf16x3(const ConvParams p) {
     const int rem = KT - tg * TPC;
     return rem < TPC ? rem : TPC;
   };
-  // ---- weight slab: global -> LDS by LDS-DMA, only the taps that exist ----
+  // ---- weight slab: global -> LDS by LDS-DMA, PW pieces per thread (whole slab:
+  // the packer zero-fills the taps past KT, so every thread issues the same count) ----
   auto issue_w = [&](int c, __bf16* Ws) {
     const __bf16* src = wsrc + (int64_t)c * SLAB;
-    const int n16 = taps_in(c) * TAP_ELEMS / 8;  // 16-B pieces
-    for (int i = wave; i * 64 < n16; i += NW) {
-      const int piece = i * 64 + lane;
-      if (piece < n16)
-        __builtin_amdgcn_global_load_lds((gptr_t1)(src + piece * 8), (lds_ptr_t3)(Ws + i * 512),
-                                         16, 0, 0);
+#pragma unroll
+    for (int q = 0; q < PW; ++q) {
+      const int i = wave + q * NW;
+      __builtin_amdgcn_global_load_lds((gptr_t1)(src + (i * 64 + lane) * 8),
+                                       (lds_ptr_t3)(Ws + i * 512), 16, 0, 0);
     }
   };
-  // ---- activations: task = (window row t, 8 channels), 32-bit offsets from xb ----
   // raw loads (clamped offsets) into registers; the zero padding is applied at store
   // time from a bit mask, so the loads' latency hides behind the chunk's MFMAs
   float xv[XQ][8];
@@ -191,40 +208,79 @@ conv1d_bf16x3(const ConvParams p) {
       }
   };
 
-  // ---- prologue: weight slab of chunk 0, input window of channel group 0 ----
-  issue_w(0, Wbuf0);
+  // ---- prologue: weight slabs of chunks 0..WD-2, input window of channel group 0 ----
   load_x(0);
+#pragma unroll
+  for (int c = 0; c < WD - 1; ++c)
+    if (c < p.n_chunks) issue_w(c, Wbuf0 + c * SLAB);
   store_x(Xbuf0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
+  wait_vm<0>();
+  lds_barrier();
 
-  // chunk c = (channel group g, tap group tg); weights double-buffered per chunk,
-  // the input window double-buffered per channel group (staged once for all taps)
+  // chunk c = (channel group g, tap group tg).  Weights: a ring of WD slabs, chunk c+WD-1
+  // issued while chunk c is multiplied.  Input window: double-buffered per channel
+  // group; group g+1's loads are issued at tap group xg = max(n_tg-2, 0) of group g
+  // and land in LDS at the group's last tap group.
+  const int xg = n_tg >= 2 ? n_tg - 2 : 0;
+  int wslot = 0;                                  // ring slot of chunk c
   for (int c = 0; c < p.n_chunks; ++c) {
     const int g = c / n_tg, tg = c - (c / n_tg) * n_tg;
-    const __bf16* Ws = Wbuf0 + (c & 1) * SLAB;
+    const __bf16* Ws = Wbuf0 + wslot * SLAB;
     const __bf16* Xh = Xbuf0 + (g & 1) * xbuf;
-    const bool has_next = c + 1 < p.n_chunks;
-    const bool next_group = has_next && tg == n_tg - 1;
-    if (has_next && !(p.dbg & 2)) issue_w(c + 1, Wbuf0 + ((c + 1) & 1) * SLAB);
-    const bool stage_x = next_group && !(p.dbg & 1);
-    if (stage_x) load_x(g + 1);
+    const bool more_groups = (g + 1) * n_tg < p.n_chunks;
+    const bool issue_x = more_groups && tg == xg && !(p.dbg & 1);
+    const bool store_now = more_groups && tg == n_tg - 1 && !(p.dbg & 1);
+    // always PW pieces per thread, so every vmcnt below is a constant: past the last
+    // chunk the last slab is re-read into the free slot (that of chunk c-1)
+    auto issue_next_w = [&]() {
+      int s2 = wslot + WD - 1;
+      if (s2 >= WD) s2 -= WD;
+      issue_w(min(c + WD - 1, p.n_chunks - 1), Wbuf0 + s2 * SLAB);
+    };
+    // with a deeper ring, the chunk that stores the next input window issues its slab
+    // after that store: the compiler's vmcnt(0) for the input registers then does not
+    // also wait for the new slab
+    const bool w_late = WD > 2 && store_now;
+    if (!w_late) issue_next_w();
+    if (issue_x) load_x(g + 1);  // after the slab DMA: a vmcnt can wait for it, not for these
     const int nt = taps_in(c);
     const int tap0 = tg * TPC;
     Frag f0, f1;
-    load_frag(Ws, Xh, 0, tap0, f0);
+    (void)f1;
+    if constexpr (WM * WN >= 8) {
+      // 64x128 per wave: one fragment set in flight (the accumulators hold 128 VGPRs)
 #pragma unroll
-    for (int jj = 0; jj < TPC; jj += 2) {
-      if (jj < nt) {
-        if (jj + 1 < nt) load_frag(Ws, Xh, jj + 1, tap0 + jj + 1, f1);
-        mma(f0);
-        if (jj + 2 < nt) load_frag(Ws, Xh, jj + 2, tap0 + jj + 2, f0);
-        if (jj + 1 < nt) mma(f1);
+      for (int jj = 0; jj < TPC; ++jj) {
+        if (jj < nt) {
+          load_frag(Ws, Xh, jj, tap0 + jj, f0);
+          mma(f0);
+        }
+      }
+    } else {
+      load_frag(Ws, Xh, 0, tap0, f0);
+#pragma unroll
+      for (int jj = 0; jj < TPC; jj += 2) {
+        if (jj < nt) {
+          if (jj + 1 < nt) load_frag(Ws, Xh, jj + 1, tap0 + jj + 1, f1);
+          mma(f0);
+          if (jj + 2 < nt) load_frag(Ws, Xh, jj + 2, tap0 + jj + 2, f0);
+          if (jj + 1 < nt) mma(f1);
+        }
       }
     }
-    if (stage_x) store_x(Xbuf0 + ((g + 1) & 1) * xbuf);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
+    if (store_now) store_x(Xbuf0 + ((g + 1) & 1) * xbuf);
+    if (w_late) issue_next_w();
+    // the slab of chunk c+1 must have landed.  Younger than it: the slabs of chunks
+    // c+2..c+WD-1 (PW pieces each) and this chunk's input loads when a later chunk
+    // consumes them.
+    if (issue_x && !store_now) wait_vm<NX + PW * (WD - 2)>();
+    else wait_vm<PW * (WD - 2)>();
+    if (!(p.dbg & 4)) lds_barrier();
+    if (++wslot == WD) wslot = 0;
+  }
+  if (p.dbg & 8) {  // ablation: no epilogue
+    if (acc[0][0][0] == 1.2345e-30f) p.y[0] = acc[WM - 1][WN - 1][15];
+    return;
   }
 
   // ---- epilogue (same contract as conv1d_mfma_f32) ----
@@ -265,7 +321,7 @@ template <int KT, int TILE, bool UPS>
 struct Inst3 {
   static constexpr Bf16x3Cfg t = kBf16x3Tiles[TILE];
   static ConvFn3 fn() {
-    return conv1d_bf16x3<KT, t.TPC, t.WAVES_M, t.WAVES_N, t.WM, t.WN, UPS>;
+    return conv1d_bf16x3<KT, t.TPC, t.WAVES_M, t.WAVES_N, t.WM, t.WN, t.WD, UPS>;
   }
 };
 
@@ -280,7 +336,8 @@ struct Entry3 {
 
 #define HFG3_ENTRY(KT, TILE, UPS) \
   { KT, TILE, UPS, Inst3<KT, TILE, UPS>::fn(), false, {0} }
-#define HFG3_TILES(KT, UPS) HFG3_ENTRY(KT, 0, UPS), HFG3_ENTRY(KT, 1, UPS), HFG3_ENTRY(KT, 2, UPS)
+#define HFG3_TILES(KT, UPS) \
+  HFG3_ENTRY(KT, 0, UPS), HFG3_ENTRY(KT, 1, UPS), HFG3_ENTRY(KT, 2, UPS), HFG3_ENTRY(KT, 3, UPS)
 
 Entry3 g_entries3[] = {
     HFG3_TILES(3, false), HFG3_TILES(5, false), HFG3_TILES(7, false), HFG3_TILES(11, false),
@@ -294,7 +351,7 @@ size_t bf16x3_lds_bytes(int tile, int kt, int dil) {
   const size_t slab = (size_t)t.TPC * 2 * t.MT() * 16;  // bf16: taps x planes x rows x 16 ch
   const int xw = t.NTILE() + (kt - 1) * dil;
   const size_t xplane = ((size_t)xw * 16 + 7) & ~(size_t)7;
-  return sizeof(__bf16) * (2 * slab + 2 * 2 * xplane);  // 2 weight slabs + 2 (hi,lo) windows
+  return sizeof(__bf16) * (t.WD * slab + 2 * 2 * xplane);  // weight ring + 2 (hi,lo) windows
 }
 
 hipError_t launch_conv_bf16x3(int tile, int kt, bool ups, const ConvParams& p, int n_tiles,

@@ -95,6 +95,7 @@ struct hfg_handle {
   void* ws = nullptr;
   size_t ws_bytes = 0;
   bool profiling = false;
+  int big_tile = 3;   // bf16x3 tile for M >= 128 (HFG_BF16X3_BIGTILE env: 0 or 3)
   int dbg_flags = 0;  // HFG_DEBUG_FLAGS env (kernel ablations; wrong results when set)
   std::vector<ProfRec> prof;
   std::vector<hipEvent_t> event_pool;
@@ -222,9 +223,9 @@ void build_layers(hfg_handle* h) {
     if (h->cfg.dtype == HFG_DTYPE_BF16X3 && (L.kind == L_CONV || L.kind == L_UPS) &&
         hfg::bf16x3_tile_for_rows(L.M) >= 0) {
       // split-precision path: chunk = 16 channels x TPC taps
-      const hfg::Bf16x3Cfg& t3 = hfg::kBf16x3Tiles[hfg::bf16x3_tile_for_rows(L.M)];
+      L.tile = hfg::bf16x3_tile_for_rows(L.M, h->big_tile);
+      const hfg::Bf16x3Cfg& t3 = hfg::kBf16x3Tiles[L.tile];
       L.prec = 1;
-      L.tile = hfg::bf16x3_tile_for_rows(L.M);
       L.CK = hfg::kBf16x3Ck;
       L.m_tiles = (L.M + t3.MT() - 1) / t3.MT();
       L.n_chunks = ((L.C_in + L.CK - 1) / L.CK) * ((L.KT + t3.TPC - 1) / t3.TPC);
@@ -682,6 +683,10 @@ int hfg_create(const hfg_config* cfg, int device, hfg_handle** out) {
   h->cfg = *cfg;
   h->device = device;
   if (const char* dbg = getenv("HFG_DEBUG_FLAGS")) h->dbg_flags = atoi(dbg);
+  if (const char* bt = getenv("HFG_BF16X3_BIGTILE")) {
+    const int v = atoi(bt);
+    if (v == 0 || v == 3) h->big_tile = v;
+  }
   build_layers(h);
   *out = h;
   return HFG_OK;

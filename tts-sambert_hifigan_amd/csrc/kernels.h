@@ -36,8 +36,9 @@ struct ConvParams {
   float mrf_div;
   int ups_s, ups_p, L_out;  // UPS store mapping
   int n_chunks;      // ceil(C_in / CK)
-  int dbg;           // ablation flags (HFG_DEBUG_FLAGS; 0 in production): bit0 skip input
-                     // restaging after the first chunk, bit1 skip weight restaging
+  int dbg;           // ablation flags (HFG_DEBUG_FLAGS; 0 in production; wrong results when
+                     // set), bf16x3 kernel: bit0 skip input restaging after the first
+                     // chunk, bit2 no per-chunk barrier, bit3 no epilogue
 };
 
 // Tile configurations of conv1d_mfma_f32 (fp32 MFMA 32x32x2).
@@ -84,21 +85,24 @@ constexpr int kMaxDil = 16;
 constexpr int halo_max(int dkt) { return dkt == 0 ? 192 : (dkt - 1) * kMaxDil; }
 
 // ---- split-precision bf16x3 conv (conv_bf16x3.hip) ----
-// B0 = 128 x 256 (2x4 waves of 64x64, 4 taps per chunk, 1 block per CU),
-// B1 = 64 x 256 (1x4 waves of 64x64, 2 taps per chunk, 2 blocks per CU),
-// B2 = 32 x 256 (1x4 waves of 32x64, 4 taps per chunk, 2 blocks per CU).
+// WD = depth of the weight-slab ring (chunks in flight: WD - 1).
 struct Bf16x3Cfg {
-  int WAVES_M, WAVES_N, WM, WN, TPC;
+  int WAVES_M, WAVES_N, WM, WN, TPC, WD;
   constexpr int MT() const { return 32 * WM * WAVES_M; }
   constexpr int NTILE() const { return 32 * WN * WAVES_N; }
   constexpr int threads() const { return 64 * WAVES_M * WAVES_N; }
 };
-constexpr int kBf16x3Tiles_n = 3;
+constexpr int kBf16x3Tiles_n = 4;
+// 0: 128x256, 2x4 waves of 64x64, 4 taps/chunk, 3-deep weight ring (1 block/CU)
+// 1: 64x256, 1x4 waves of 64x64, 2 taps/chunk (2 blocks/CU)
+// 2: 32x256, 1x4 waves of 32x64, 4 taps/chunk (2 blocks/CU)
+// 3: 128x256, 2x2 waves of 64x128, 2 taps/chunk (2 blocks/CU: one block's epilogue
+//    overlaps the other's main loop)
 constexpr Bf16x3Cfg kBf16x3Tiles[kBf16x3Tiles_n] = {
-    {2, 4, 2, 2, 4}, {1, 4, 2, 2, 2}, {1, 4, 1, 2, 4}};
+    {2, 4, 2, 2, 4, 3}, {1, 4, 2, 2, 2, 2}, {1, 4, 1, 2, 4, 2}, {2, 2, 2, 4, 2, 2}};
 constexpr int kBf16x3Ck = 16;  // channels per chunk (one MFMA k-step per tap)
-inline int bf16x3_tile_for_rows(int M) {
-  return M >= 128 ? 0 : (M >= 64 ? 1 : (M >= 32 ? 2 : -1));
+inline int bf16x3_tile_for_rows(int M, int big_tile = 0) {
+  return M >= 128 ? big_tile : (M >= 64 ? 1 : (M >= 32 ? 2 : -1));
 }
 size_t bf16x3_lds_bytes(int tile, int kt, int dil);
 hipError_t launch_conv_bf16x3(int tile, int kt, bool ups, const ConvParams& p, int n_tiles,
