@@ -288,7 +288,7 @@ def test_bf16x3_polyphase_upsampler_packing(pkg):
     for k, v in sd.items():
         h.set_weight(k, torch.from_numpy(v))
     h.commit()
-    waves = {0: (2, 2, 4), 1: (1, 2, 2), 2: (1, 1, 4)}
+    waves = {0: (2, 2, 4), 1: (1, 2, 2), 2: (1, 1, 4), 3: (2, 2, 2)}
     rng = np.random.default_rng(1)
     c0 = cfg.upsample_initial_channel
     for i, (u, k) in enumerate(zip(cfg.upsample_rates, cfg.upsample_kernel_sizes)):
