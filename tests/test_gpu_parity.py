@@ -95,13 +95,15 @@ def test_golden_fixture_bf16x3(pkg, golden_index, name):
     assert rel < 1e-3, rel
 
 
-@pytest.mark.parametrize("big_tile", ["0", "3"])
+@pytest.mark.parametrize("big_tile,pair", [("0", "1"), ("3", "1"), ("3", "0")])
 @pytest.mark.parametrize("preset,B,T", [("v1", 2, 300), ("v2star", 2, 200)])
-def test_bf16x3_vs_oracle_longer(pkg, preset, B, T, big_tile, monkeypatch):
+def test_bf16x3_vs_oracle_longer(pkg, preset, B, T, big_tile, pair, monkeypatch):
     """Random weights/mel vs the oracle, with each tile choice for the M >= 128 layers
-    (HFG_BF16X3_BIGTILE: 0 = 128x256 8-wave, 3 = 128x128 4-wave)."""
+    (HFG_BF16X3_BIGTILE: 0 = 128x256 8-wave, 3 = 128x256 4-wave) and with the fused
+    ResBlock-step kernel for C in {32, 64} on (HFG_PAIR=1, default) or off."""
     from oracle import config as C, prng
     monkeypatch.setenv("HFG_BF16X3_BIGTILE", big_tile)
+    monkeypatch.setenv("HFG_PAIR", pair)
     dev = _dev()
     cfg = C.PRESETS[preset]
     sd = C.make_state_dict(cfg, seed=7)

@@ -1,0 +1,34 @@
+// bf16x3_common.h — pieces shared by the split-precision conv kernels
+// (conv_bf16x3.hip: one Conv1d / polyphase ConvTranspose1d per launch;
+//  conv_pair_bf16x3.hip: a whole ResBlock dilation step conv1 -> conv2 per launch).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include "epilogue.h"
+#include "kernels.h"
+
+namespace hfg {
+
+typedef floatx16e floatx16;
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __attribute__((address_space(3))) void* lds_ptr_t3;
+typedef __attribute__((address_space(1))) void* gptr_t1;
+
+__device__ __forceinline__ float lrelu3(float v) { return v > 0.f ? v : v * kLReluSlope; }
+
+// s_waitcnt vmcnt(N) with a compile-time N
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+// workgroup barrier over LDS writes made by ds_write (lgkmcnt): the caller has already
+// waited (vmcnt) for the LDS-DMA pieces the next chunk reads.  Written as one asm block
+// so no fence makes the compiler wait for every outstanding global load / LDS-DMA
+// piece, and the "memory" clobber keeps LDS accesses on their side of the barrier.
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+}  // namespace hfg

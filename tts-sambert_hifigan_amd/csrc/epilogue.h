@@ -18,16 +18,16 @@ namespace hfg {
 typedef float floatx16e __attribute__((ext_vector_type(16)));
 
 template <int WM, int WN>
-__device__ __forceinline__ void conv_epilogue(const ConvParams& p, floatx16e (&acc)[WM][WN],
-                                              int b, int row_base, int n_base, int N_b,
-                                              int half, int col) {
+__device__ __forceinline__ void conv_epilogue(const ConvParams& p, const float* __restrict__ bias,
+                                              floatx16e (&acc)[WM][WN], int b, int row_base,
+                                              int n_base, int N_b, int half, int col) {
   const int64_t bo = (int64_t)b * p.y_bs;
   const char* resb = p.res ? reinterpret_cast<const char*>(p.res + bo) : nullptr;
   char* outb = reinterpret_cast<char*>((p.mrf ? p.mrf : p.y) + bo);
   const bool add_mrf = p.mrf && (p.mrf_mode & 1);
   const bool div_mrf = p.mrf && (p.mrf_mode & 2);
   const bool act = p.act_out != 0;
-  const float* __restrict__ bias = p.bias;  // padded to the m-tile: every row index is readable
+  // bias: padded to the m-tile, every row index is readable
 #pragma unroll
   for (int i = 0; i < WM; ++i) {
     float bv[16];
@@ -75,6 +75,13 @@ __device__ __forceinline__ void conv_epilogue(const ConvParams& p, floatx16e (&a
         if (ok[r]) *reinterpret_cast<float*>(outb + off[r]) = v[r];
     }
   }
+}
+
+template <int WM, int WN>
+__device__ __forceinline__ void conv_epilogue(const ConvParams& p, floatx16e (&acc)[WM][WN],
+                                              int b, int row_base, int n_base, int N_b,
+                                              int half, int col) {
+  conv_epilogue<WM, WN>(p, p.bias, acc, b, row_base, n_base, N_b, half, col);
 }
 
 }  // namespace hfg

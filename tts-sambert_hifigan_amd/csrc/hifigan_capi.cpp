@@ -96,6 +96,8 @@ struct hfg_handle {
   size_t ws_bytes = 0;
   bool profiling = false;
   int big_tile = 3;   // bf16x3 tile for M >= 128 (HFG_BF16X3_BIGTILE env: 0 or 3)
+  bool use_pair = false;  // fused ResBlock steps for C in {32, 64} (HFG_PAIR=1 enables; slower
+                         // than two launches on MI355X as of r01)
   int dbg_flags = 0;  // HFG_DEBUG_FLAGS env (kernel ablations; wrong results when set)
   std::vector<ProfRec> prof;
   std::vector<hipEvent_t> event_pool;
@@ -517,6 +519,51 @@ int run_conv(hfg_handle* h, Launcher& ln, const Layer& L, const float* x, int64_
   return HFG_OK;
 }
 
+// One ResBlock dilation step (conv1 -> conv2, residual, optional MRF) in one launch.
+// y must not alias x: neighbouring blocks still read x's halo while this one stores.
+int run_pair(hfg_handle* h, Launcher& ln, const Layer& L1, const Layer& L2, const float* x,
+             int64_t B, int64_t Lt, float* y, float* mrf, int mrf_mode, float mrf_div,
+             const int32_t* lens) {
+  ConvParams p{};
+  p.x = x;
+  p.x_bs = (int64_t)L1.C_in * Lt;
+  p.x_cs = Lt;
+  p.x_ts = 1;
+  p.C_in = L1.C_in;
+  p.L_in = (int)Lt;
+  p.len_in = lens;
+  p.len_out = lens;
+  p.w = h->packed_dev + L1.w_off;
+  p.bias = h->packed_dev + L1.b_off;
+  p.w2 = h->packed_dev + L2.w_off;
+  p.bias2 = h->packed_dev + L2.b_off;
+  p.y = y;
+  p.y_bs = (int64_t)L2.C_out * Lt;
+  p.M = L2.M;
+  p.N = (int)Lt;
+  p.dil = L1.dil;
+  p.kt = L1.KT;
+  p.act_in = 1;
+  p.act_out = 0;
+  p.res = x;
+  p.mrf = mrf;
+  p.mrf_mode = mrf_mode;
+  p.mrf_div = mrf_div;
+  p.n_chunks = L1.n_chunks;
+  p.dbg = h->dbg_flags;
+  const int n_tiles = (int)((Lt + hfg::pair_tile_cols(L1.KT) - 1) / hfg::pair_tile_cols(L1.KT));
+  const double flop = 2.0 * 2.0 * L1.C_out * L1.C_in * L1.k * (double)Lt * B;
+  double bytes = 4.0 * B * Lt * (L1.C_in + L2.C_out) + 2 * 4.0 * L1.C_out * L1.C_in * L1.k;
+  if (mrf && (mrf_mode & 1)) bytes += 4.0 * B * Lt * L2.C_out;
+  const char* name = nullptr;
+  ln.begin(flop, bytes);
+  hipError_t e = hfg::launch_pair_bf16x3(L1.tile, L1.KT, p, n_tiles, (int)B, ln.stream, &name);
+  ln.end(name);
+  if (e != hipSuccess)
+    return fail(HFG_EIO, "launch pair %s: %s", L1.mod.c_str(), hipGetErrorString(e));
+  return HFG_OK;
+}
+
 int run_ups(hfg_handle* h, Launcher& ln, const Layer& L, const float* x, int64_t B, int64_t Lin,
             int64_t Lout, float* y, const int32_t* len_in, const int32_t* len_out) {
   ConvParams p{};
@@ -618,10 +665,26 @@ int forward_impl(hfg_handle* h, const float* mel, int64_t B, int64_t T, const hf
     // MRF (models/hifigan.py:116-131) of ResBlocks (:72-86)
     int idx = 0;
     for (int j = 0; j < c.n_res; ++j) {
+      const float* psrc = X;  // fused path: ping-pong R / Tb (a pair may not write its input)
       for (int m = 0; m < c.n_dil[j]; ++m, ++idx) {
         const float* src = (m == 0) ? X : R;
         const Layer& L1 = h->layers[st.conv1[idx]];
         const Layer& L2 = h->layers[st.conv2[idx]];
+        if (h->use_pair && L1.prec == 1 && L2.prec == 1 && L2.KT == L1.KT && L2.dil == 1 &&
+            L2.tile == L1.tile && hfg::pair_supported(L1.tile, L1.m_tiles, L1.KT, L1.dil)) {
+          const bool last = (m == c.n_dil[j] - 1);
+          if (!last) {
+            float* dst = (m % 2 == 0) ? R : Tb;
+            rc = run_pair(h, ln, L1, L2, psrc, B, L, dst, nullptr, 0, 1.f, lens_at(i + 1));
+            psrc = dst;
+          } else {
+            int mode = (j > 0 ? 1 : 0) | (j == c.n_res - 1 ? 2 : 0);
+            rc = run_pair(h, ln, L1, L2, psrc, B, L, nullptr, MRF, mode, (float)c.n_res,
+                          lens_at(i + 1));
+          }
+          if (rc) return rc;
+          continue;
+        }
         // xt = lrelu(conv1(lrelu(x)))
         rc = run_conv(h, ln, L1, src, B, L, Tb, true, true, nullptr, nullptr, 0, 1.f,
                       lens_at(i + 1));
@@ -687,6 +750,7 @@ int hfg_create(const hfg_config* cfg, int device, hfg_handle** out) {
     const int v = atoi(bt);
     if (v == 0 || v == 3) h->big_tile = v;
   }
+  if (const char* pe = getenv("HFG_PAIR")) h->use_pair = atoi(pe) != 0;
   build_layers(h);
   *out = h;
   return HFG_OK;

@@ -36,6 +36,8 @@ struct ConvParams {
   float mrf_div;
   int ups_s, ups_p, L_out;  // UPS store mapping
   int n_chunks;      // ceil(C_in / CK)
+  const float* w2;   // ResBlock pair kernel: conv2's packed weights / bias (conv1 in w, bias)
+  const float* bias2;
   int dbg;           // ablation flags (HFG_DEBUG_FLAGS; 0 in production; wrong results when
                      // set), bf16x3 kernel: bit0 skip input restaging after the first
                      // chunk, bit2 no per-chunk barrier, bit3 no epilogue
@@ -107,6 +109,19 @@ inline int bf16x3_tile_for_rows(int M, int big_tile = 0) {
 size_t bf16x3_lds_bytes(int tile, int kt, int dil);
 hipError_t launch_conv_bf16x3(int tile, int kt, bool ups, const ConvParams& p, int n_tiles,
                               int m_tiles, int batch, hipStream_t stream, const char** name);
+
+// ---- fused ResBlock dilation step (conv_pair_bf16x3.hip) ----
+// out = x + conv2(lrelu(conv1(lrelu(x)))) (models/hifigan.py:79-85) in one launch for
+// C in {32, 64}: conv1's output never leaves LDS.  Uses the bf16x3 packing of tile 1
+// (C = 64) or tile 2 (C = 32); a block computes pair_tile_cols(tile, k) outputs.
+constexpr int kPairCols = 128;  // GEMM columns per phase (4 waves x 32)
+inline bool pair_supported(int tile, int m_tiles, int kt, int dil) {
+  return (tile == 1 || tile == 2) && m_tiles == 1 && kt >= 1 && kt <= 16 && dil <= kMaxDil;
+}
+inline int pair_tile_cols(int kt) { return kPairCols - (kt - 1); }
+size_t pair_lds_bytes(int tile, int kt, int dil);
+hipError_t launch_pair_bf16x3(int tile, int kt, const ConvParams& p, int n_tiles, int batch,
+                              hipStream_t stream, const char** name);
 
 // Launch the conv kernel for (tile, taps, ups).  Returns a hipError_t and,
 // via *name, the kernel's template-instance name (as rocprofv3 prints it).
