@@ -25,6 +25,14 @@ extern "C" {
 int hfg_debug_packed_layer(hfg_handle* h, const char* mod, float* out, size_t cap,
                            int64_t* info);
 
+/* Packed image of the whole-ResBlock launch of stage `stage`, ResBlock `j`
+ * (resblock_bf16x3.hip; bf16x3 handles, stages with 32 or 64 channels):
+ * w_len floats of A stream (bf16 hi/lo pairs) followed by b_len biases.
+ * info[8] receives {fused (0/1), C, KT, n_conv, halo, W, w_len, b_len}.
+ * Returns HFG_OK with info[0] = 0 when the stage runs layer by layer. */
+int hfg_debug_packed_resblock(hfg_handle* h, int stage, int j, float* out, size_t cap,
+                              int64_t* info);
+
 #ifdef __cplusplus
 }
 #endif

@@ -31,7 +31,7 @@ def header_symbols():
 def test_library_exports_every_header_symbol(pkg):
     lib = pkg.load_library()
     syms = header_symbols()
-    assert len(syms) == 24
+    assert len(syms) == 25
     for s in sorted(syms):
         assert hasattr(lib, s), f"missing export {s}"
     assert set(syms) == set(pkg._lib.SIGNATURES), "ctypes signatures out of sync with headers"
@@ -310,3 +310,97 @@ def test_bf16x3_polyphase_upsampler_packing(pkg):
             y[co, t[ok]] = g[m, ok]
         assert not np.isnan(y).any()
         assert np.abs(y - ref).max() < 1e-3 * np.abs(ref).max()
+
+
+def _lrelu(v):
+    return np.where(v > 0, v, 0.1 * v)
+
+
+def _conv_same(x, w, b, d):
+    """Conv1d with 'same' zero padding (k odd), float64: x [C, L], w [C, C, k]."""
+    k = w.shape[2]
+    pad = (k - 1) // 2 * d
+    xp = np.pad(x, ((0, 0), (pad, pad)))
+    L = x.shape[1]
+    out = np.repeat(b[:, None], L, axis=1).astype(np.float64)
+    for j in range(k):
+        out += w[:, :, j] @ xp[:, j * d:j * d + L]
+    return out
+
+
+@pytest.mark.parametrize("preset", ["v1", "v2star"])
+def test_resblock_stream_packing_and_windowing(pkg, preset):
+    """Whole-ResBlock launches (resblock_bf16x3.hip) of the narrow stages: the packed A
+    stream decodes (hi + lo, permuted channel slots) to every conv's weights, and the
+    kernel's windowing (NWIN-column windows, garbage edges, centre W = NWIN - 2*halo,
+    zero outside [0, len)) reproduces the un-windowed ResBlock, emulated in float64."""
+    cfg = C.PRESETS[preset]
+    sd = C.make_state_dict(cfg, seed=43)
+    h = host_handle(pkg, cfg, "bf16x3")
+    for k, v in sd.items():
+        h.set_weight(k, torch.from_numpy(v))
+    h.commit()
+    n_fused = 0
+    for i in range(len(cfg.upsample_rates)):
+        for j in range(len(cfg.resblock_kernel_sizes)):
+            info, packed, bias = h.packed_resblock(i, j)
+            Cst = cfg.upsample_initial_channel >> (i + 1)
+            if not info["fused"]:
+                assert Cst not in (32, 64) or preset != "v1"
+                continue
+            n_fused += 1
+            Cc, KT, n_conv = info["C"], info["KT"], info["n_conv"]
+            assert Cc == Cst and KT == cfg.resblock_kernel_sizes[j]
+            dils = cfg.resblock_dilation_sizes[j]
+            assert n_conv == 2 * len(dils)
+            assert info["halo"] == sum((KT - 1) // 2 * d + (KT - 1) // 2 for d in dils)
+            nwin = info["W"] + 2 * info["halo"]
+            assert nwin in (512, 1024)
+            # decode [wave_m][conv][g][tap][plane][lane][8]
+            u = packed.view(np.uint16).reshape(Cc // 32, n_conv, Cc // 16, KT, 2, 64, 8)
+            val = bf2f(u[:, :, :, :, 0]).astype(np.float64) + bf2f(u[:, :, :, :, 1])
+            lane = np.arange(64)
+            Ws = []
+            for e in range(n_conv):
+                m, second = divmod(e, 2)
+                mod = f"mrfs.{i}.resblocks.{j}.convs{2 if second else 1}.{m}"
+                W = sd[mod + ".weight"].astype(np.float64)
+                rec = np.zeros_like(W)
+                for wm in range(Cc // 32):
+                    rows = wm * 32 + (lane & 31)
+                    for g in range(Cc // 16):
+                        for el in range(8):
+                            ci = g * 16 + 4 * (lane >> 5) + (el & 3) + 8 * (el >> 2)
+                            rec[rows, ci, :] = val[wm, e, g, :, lane, el]
+                assert np.abs(rec - W).max() <= 2.0 ** -15 * np.abs(W).max(), mod
+                assert np.array_equal(bias[e * Cc:(e + 1) * Cc], sd[mod + ".bias"])
+                Ws.append((rec, sd[mod + ".bias"].astype(np.float64)))
+            # windowed emulation vs direct, on one short utterance (len < L)
+            if j != len(cfg.resblock_kernel_sizes) - 1:
+                continue
+            rng = np.random.default_rng(5)
+            L, ln = 3 * info["W"] // 2 + 37, 3 * info["W"] // 2 + 5
+            x = rng.standard_normal((Cc, L))
+            x[:, ln:] = 0.0
+
+            def resblock(xx, valid):
+                for m in range(len(dils)):
+                    (w1, b1), (w2, b2) = Ws[2 * m], Ws[2 * m + 1]
+                    t = _lrelu(_conv_same(_lrelu(xx) * valid, w1, b1, dils[m])) * valid
+                    xx = xx + _conv_same(t, w2, b2, 1)
+                return xx
+
+            direct = resblock(x[:, :ln], np.ones(ln))
+            out = np.zeros((Cc, ln))
+            for t0 in range(0, ln, info["W"]):
+                ws = t0 - info["halo"]
+                cols = ws + np.arange(nwin)
+                valid = ((cols >= 0) & (cols < ln)).astype(np.float64)
+                xw = np.where(valid > 0, x[:, np.clip(cols, 0, L - 1)], 0.0)
+                # edges see arbitrary data past the window: emulate with zero padding of the
+                # window itself (any value gives the same centre)
+                yw = resblock(xw, valid)
+                c0, c1 = info["halo"], info["halo"] + min(info["W"], ln - t0)
+                out[:, t0:t0 + (c1 - c0)] = yw[:, c0:c1]
+            assert np.abs(out - direct).max() < 1e-9
+    assert n_fused >= (6 if preset == "v1" else 1)

@@ -95,15 +95,17 @@ def test_golden_fixture_bf16x3(pkg, golden_index, name):
     assert rel < 1e-3, rel
 
 
-@pytest.mark.parametrize("big_tile,pair", [("0", "1"), ("3", "1"), ("3", "0")])
+@pytest.mark.parametrize("big_tile,fused,wn32", [("0", "1", "8"), ("3", "1", "4"), ("3", "0", "8")])
 @pytest.mark.parametrize("preset,B,T", [("v1", 2, 300), ("v2star", 2, 200)])
-def test_bf16x3_vs_oracle_longer(pkg, preset, B, T, big_tile, pair, monkeypatch):
+def test_bf16x3_vs_oracle_longer(pkg, preset, B, T, big_tile, fused, wn32, monkeypatch):
     """Random weights/mel vs the oracle, with each tile choice for the M >= 128 layers
-    (HFG_BF16X3_BIGTILE: 0 = 128x256 8-wave, 3 = 128x256 4-wave) and with the fused
-    ResBlock-step kernel for C in {32, 64} on (HFG_PAIR=1, default) or off."""
+    (HFG_BF16X3_BIGTILE: 0 = 128x256 8-wave, 3 = 128x256 4-wave) and with the
+    whole-ResBlock kernel for C in {32, 64} on (HFG_FUSED_RB=1, default; C = 32 window
+    512 or 1024 columns) or off (layer per launch)."""
     from oracle import config as C, prng
     monkeypatch.setenv("HFG_BF16X3_BIGTILE", big_tile)
-    monkeypatch.setenv("HFG_PAIR", pair)
+    monkeypatch.setenv("HFG_FUSED_RB", fused)
+    monkeypatch.setenv("HFG_RB_WN32", wn32)
     dev = _dev()
     cfg = C.PRESETS[preset]
     sd = C.make_state_dict(cfg, seed=7)
@@ -111,5 +113,30 @@ def test_bf16x3_vs_oracle_longer(pkg, preset, B, T, big_tile, pair, monkeypatch)
     wav = _run(_gen(pkg, cfg, sd, dev, precision="bf16x3"), mel, dev)
     ref = _oracle(cfg, sd, mel)
     err = np.abs(wav - ref).max()
-    print(f"{preset} B={B} T={T} [bf16x3]: max err {err:.3e}")
+    print(f"{preset} B={B} T={T} [bf16x3 fused={fused}]: max err {err:.3e}")
     assert err < ATOL
+
+
+@pytest.mark.parametrize("wn32", ["4", "8"])
+def test_fused_resblock_matches_layer_path(pkg, wn32, monkeypatch):
+    """Whole-ResBlock kernel vs the layer-per-launch bf16x3 schedule on a ragged batch
+    long enough for many windows per utterance (window seams, lengths that end inside
+    a window, an utterance shorter than one window)."""
+    from oracle import config as C, prng
+    dev = _dev()
+    cfg = C.V1
+    sd = C.make_state_dict(cfg, seed=21)
+    B, T = 4, 160
+    mel = torch.as_tensor(prng.mel_input(21, (B, cfg.n_mels, T))).to(dev)
+    lens = torch.tensor([160, 97, 3, 131], dtype=torch.int32, device=dev)
+    outs = []
+    for fused in ("0", "1"):
+        monkeypatch.setenv("HFG_FUSED_RB", fused)
+        monkeypatch.setenv("HFG_RB_WN32", wn32)
+        gen = _gen(pkg, cfg, sd, dev, precision="bf16x3")
+        with torch.no_grad():
+            outs.append(gen(mel, lengths=lens).cpu().numpy())
+        torch.cuda.synchronize()
+    err = np.abs(outs[0] - outs[1]).max()
+    print(f"fused vs layer path (wn32={wn32}): max diff {err:.3e}")
+    assert err < 2e-5

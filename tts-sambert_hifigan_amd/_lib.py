@@ -126,6 +126,8 @@ SIGNATURES = {
     "hfg_profile_summary": (c_int, [c_void_p, c_char_p, c_size_t]),
     "hfg_debug_packed_layer": (c_int, [c_void_p, c_char_p, POINTER(c_float), c_size_t,
                                        POINTER(c_int64)]),
+    "hfg_debug_packed_resblock": (c_int, [c_void_p, c_int, c_int, POINTER(c_float), c_size_t,
+                                          POINTER(c_int64)]),
     "hfg_mel_last_error": (c_char_p, []),
     "hfg_mel_create": (c_int, [POINTER(HfgMelConfig), c_int, POINTER(c_void_p)]),
     "hfg_mel_destroy": (None, [c_void_p]),
@@ -233,3 +235,18 @@ class Handle:
             self.ptr, mod.encode(), out.ctypes.data_as(POINTER(c_float)), out.size, info))
         keys = ["kind", "M", "KT", "tile", "m_tiles", "n_chunks", "w_len", "b_len", "CK", "MT"]
         return dict(zip(keys, [int(v) for v in info])), out[:w_len], out[w_len:]
+
+    def packed_resblock(self, stage: int, j: int):
+        """(info dict, packed A stream, biases) of a whole-ResBlock launch, or
+        (info with fused=0, None, None) when the stage runs layer by layer."""
+        import numpy as np
+        info = (c_int64 * 8)()
+        check(self.lib.hfg_debug_packed_resblock(self.ptr, stage, j, None, 0, info))
+        keys = ["fused", "C", "KT", "n_conv", "halo", "W", "w_len", "b_len"]
+        d = dict(zip(keys, [int(v) for v in info]))
+        if not d["fused"]:
+            return d, None, None
+        out = np.zeros(d["w_len"] + d["b_len"], dtype=np.float32)
+        check(self.lib.hfg_debug_packed_resblock(
+            self.ptr, stage, j, out.ctypes.data_as(POINTER(c_float)), out.size, info))
+        return d, out[:d["w_len"]], out[d["w_len"]:]

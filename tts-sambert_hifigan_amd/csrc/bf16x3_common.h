@@ -1,6 +1,6 @@
 // bf16x3_common.h — pieces shared by the split-precision conv kernels
 // (conv_bf16x3.hip: one Conv1d / polyphase ConvTranspose1d per launch;
-//  conv_pair_bf16x3.hip: a whole ResBlock dilation step conv1 -> conv2 per launch).
+//  resblock_bf16x3.hip: a whole ResBlock, all dilations, per launch).
 #pragma once
 
 #include <hip/hip_runtime.h>

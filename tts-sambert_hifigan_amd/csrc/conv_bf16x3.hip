@@ -348,8 +348,8 @@ hipError_t launch_conv_bf16x3(int tile, int kt, bool ups, const ConvParams& p, i
   if (p.dil > kMaxDil || (e->kt == 0 && kt > 16)) return hipErrorInvalidValue;
   const Bf16x3Cfg& t = kBf16x3Tiles[tile];
   if (!e->name[0])
-    snprintf(e->name, sizeof(e->name), "conv1d_bf16x3<%d, %d, %d, %d, %d, %d, %s>", e->kt, t.TPC,
-             t.WAVES_M, t.WAVES_N, t.WM, t.WN, e->ups ? "true" : "false");
+    snprintf(e->name, sizeof(e->name), "conv1d_bf16x3<%d, %d, %d, %d, %d, %d, %d, %s>", e->kt,
+             t.TPC, t.WAVES_M, t.WAVES_N, t.WM, t.WN, t.WD, e->ups ? "true" : "false");
   const size_t lds = bf16x3_lds_bytes(tile, kt, p.dil);
   if (lds > 160 * 1024) return hipErrorInvalidValue;
   if (!e->attr) {

@@ -71,10 +71,20 @@ struct ProfRec {
   hipEvent_t e0, e1;
 };
 
+// One ResBlock run by resblock_bf16x3 (whole block per launch): its packed A stream
+// [wave_m][conv][group][tap][plane][lane][8] and biases [conv][C] in the packed buffer.
+struct RbFused {
+  std::vector<int> convs;     // layer indices in execution order conv1_0, conv2_0, conv1_1, ...
+  int kt = 0, halo = 0, W = 0, waves_n = 0;
+  size_t w_off = 0, w_len = 0, b_off = 0, b_len = 0;  // in floats
+};
+
 struct Stage {
   int conv_ups;               // index of the ups layer
   std::vector<int> conv1;     // [j*n_dil + m]
   std::vector<int> conv2;
+  bool fused = false;         // MRF run as one resblock_bf16x3 launch per ResBlock
+  std::vector<RbFused> rbs;
 };
 
 }  // namespace
@@ -96,8 +106,9 @@ struct hfg_handle {
   size_t ws_bytes = 0;
   bool profiling = false;
   int big_tile = 3;   // bf16x3 tile for M >= 128 (HFG_BF16X3_BIGTILE env: 0 or 3)
-  bool use_pair = false;  // fused ResBlock steps for C in {32, 64} (HFG_PAIR=1 enables; slower
-                         // than two launches on MI355X as of r01)
+  bool use_fused_rb = true;  // whole-ResBlock kernel for C in {32, 64} (HFG_FUSED_RB=0 disables)
+  int rb_waves_n32 = 4;      // window of the C = 32 ResBlock kernel: 128 * this columns
+                             // (HFG_RB_WN32: 4 or 8)
   int dbg_flags = 0;  // HFG_DEBUG_FLAGS env (kernel ablations; wrong results when set)
   std::vector<ProfRec> prof;
   std::vector<hipEvent_t> event_pool;
@@ -253,6 +264,45 @@ void build_layers(hfg_handle* h) {
     L.b_len = (size_t)L.m_tiles * t.MT();
     off += (L.b_len + 63) & ~(size_t)63;
   }
+  // whole-ResBlock launches for the narrow stages (bf16x3 only)
+  for (int i = 0; i < c.n_up; ++i) {
+    Stage& st = h->stages[i];
+    const int C = c.c0 >> (i + 1);
+    if (h->cfg.dtype != HFG_DTYPE_BF16X3 || !h->use_fused_rb || (C != 32 && C != 64)) continue;
+    const int waves_n = C == 64 ? 4 : h->rb_waves_n32;
+    const int nwin = hfg::kRbColsPerWave * waves_n;
+    std::vector<RbFused> rbs;
+    bool ok = true;
+    int idx = 0;
+    for (int j = 0; j < c.n_res && ok; ++j) {
+      RbFused rb;
+      rb.kt = c.res_kernels[j];
+      rb.waves_n = waves_n;
+      if (rb.kt % 2 == 0 || !hfg::rb_supported(C, rb.kt, waves_n) ||
+          2 * c.n_dil[j] > hfg::kRbMaxConv) {
+        ok = false;
+        break;
+      }
+      for (int m = 0; m < c.n_dil[j]; ++m, ++idx) {
+        rb.convs.push_back(st.conv1[idx]);
+        rb.convs.push_back(st.conv2[idx]);
+        rb.halo += (rb.kt - 1) / 2 * c.dil[j][m] + (rb.kt - 1) / 2;
+        if ((rb.kt - 1) / 2 * c.dil[j][m] > hfg::kRbMarg) ok = false;
+      }
+      rb.W = nwin - 2 * rb.halo;
+      if (rb.W < nwin / 4) ok = false;
+      rb.w_off = off;
+      rb.w_len = (size_t)rb.convs.size() * C * C * rb.kt;  // bf16 hi + lo = one float each
+      off += (rb.w_len + 63) & ~(size_t)63;
+      rb.b_off = off;
+      rb.b_len = rb.convs.size() * (size_t)C;
+      off += (rb.b_len + 63) & ~(size_t)63;
+      rbs.push_back(rb);
+    }
+    if (!ok) continue;  // the (unused) offsets stay reserved; harmless
+    st.fused = true;
+    st.rbs = std::move(rbs);
+  }
   h->packed_host.assign(off, 0.f);
 }
 
@@ -323,6 +373,41 @@ void pack_bf16x3(const Layer& L, F wt, uint16_t* dst) {
                   }
 }
 
+// A stream of resblock_bf16x3 (resblock_bf16x3.hip), in bf16 elements:
+//   idx = (((((wave_m*n_conv + e)*n_g + g)*KT + tap)*2 + plane)*64 + lane)*8 + el
+//   row = wave_m*32 + (lane & 31), ci = g*16 + 4*(lane >> 5) + (el & 3) + 8*(el >> 2)
+// (the permuted channel order of the kernel's operand planes); plane 0 = bf16(w),
+// plane 1 = bf16(w - hi).  Biases [conv][C].
+void pack_resblock(hfg_handle* h, const RbFused& rb) {
+  uint16_t* dst = reinterpret_cast<uint16_t*>(h->packed_host.data() + rb.w_off);
+  float* bdst = h->packed_host.data() + rb.b_off;
+  const int n_conv = (int)rb.convs.size();
+  const int C = h->layers[rb.convs[0]].C_out;
+  const int KT = rb.kt, n_g = C / 16;
+  size_t idx = 0;
+  for (int wm = 0; wm < C / 32; ++wm)
+    for (int e = 0; e < n_conv; ++e) {
+      const Layer& L = h->layers[rb.convs[e]];
+      const float* w = h->params[L.mod + ".weight"].data.data();  // [C_out][C_in][k]
+      for (int g = 0; g < n_g; ++g)
+        for (int tap = 0; tap < KT; ++tap)
+          for (int plane = 0; plane < 2; ++plane)
+            for (int lane = 0; lane < 64; ++lane)
+              for (int el = 0; el < 8; ++el) {
+                const int row = wm * 32 + (lane & 31);
+                const int ci = g * 16 + 4 * (lane >> 5) + (el & 3) + 8 * (el >> 2);
+                const float v = w[((size_t)row * C + ci) * KT + tap];
+                const uint16_t hi = f2bf(v);
+                dst[idx++] = plane == 0 ? hi : f2bf(v - bf2f(hi));
+              }
+    }
+  for (int e = 0; e < n_conv; ++e) {
+    const Layer& L = h->layers[rb.convs[e]];
+    const float* bsrc = h->params[L.mod + ".bias"].data.data();
+    for (int r = 0; r < C; ++r) bdst[(size_t)e * C + r] = bsrc[r];
+  }
+}
+
 void pack_layer(hfg_handle* h, const Layer& L) {
   const Param& W = h->params[L.mod + ".weight"];
   const Param& Bp = h->params[L.mod + ".bias"];
@@ -381,6 +466,9 @@ int do_commit(hfg_handle* h) {
     if (!h->params[key].set) return fail(HFG_EAGAIN, "weight '%s' was never set", key.c_str());
   std::fill(h->packed_host.begin(), h->packed_host.end(), 0.f);
   for (auto& L : h->layers) pack_layer(h, L);
+  for (auto& st : h->stages)
+    if (st.fused)
+      for (auto& rb : st.rbs) pack_resblock(h, rb);
   if (h->device >= 0) {
     DeviceGuard g(h->device);
     if (!g.ok) return fail(HFG_ENODEV, "hipSetDevice(%d) failed", h->device);
@@ -519,48 +607,39 @@ int run_conv(hfg_handle* h, Launcher& ln, const Layer& L, const float* x, int64_
   return HFG_OK;
 }
 
-// One ResBlock dilation step (conv1 -> conv2, residual, optional MRF) in one launch.
-// y must not alias x: neighbouring blocks still read x's halo while this one stores.
-int run_pair(hfg_handle* h, Launcher& ln, const Layer& L1, const Layer& L2, const float* x,
-             int64_t B, int64_t Lt, float* y, float* mrf, int mrf_mode, float mrf_div,
-             const int32_t* lens) {
-  ConvParams p{};
+// One whole ResBlock (all dilations) + its MRF contribution in one launch.
+int run_resblock(hfg_handle* h, Launcher& ln, const RbFused& rb, const float* x, int64_t B,
+                 int64_t Lt, float* mrf, int mrf_mode, float mrf_div, const int32_t* lens) {
+  const Layer& L0 = h->layers[rb.convs[0]];
+  const int C = L0.C_out;
+  hfg::RbParams p{};
   p.x = x;
-  p.x_bs = (int64_t)L1.C_in * Lt;
-  p.x_cs = Lt;
-  p.x_ts = 1;
-  p.C_in = L1.C_in;
-  p.L_in = (int)Lt;
-  p.len_in = lens;
-  p.len_out = lens;
-  p.w = h->packed_dev + L1.w_off;
-  p.bias = h->packed_dev + L1.b_off;
-  p.w2 = h->packed_dev + L2.w_off;
-  p.bias2 = h->packed_dev + L2.b_off;
-  p.y = y;
-  p.y_bs = (int64_t)L2.C_out * Lt;
-  p.M = L2.M;
-  p.N = (int)Lt;
-  p.dil = L1.dil;
-  p.kt = L1.KT;
-  p.act_in = 1;
-  p.act_out = 0;
-  p.res = x;
+  p.bs = (int64_t)C * Lt;
+  p.L = (int)Lt;
+  p.len = lens;
+  p.w = reinterpret_cast<const __bf16*>(h->packed_dev + rb.w_off);
+  p.w_bytes = (int)(rb.w_len * sizeof(float));
+  p.bias = h->packed_dev + rb.b_off;
+  p.n_conv = (int)rb.convs.size();
+  double flop = 0.0;
+  for (int e = 0; e < p.n_conv; ++e) {
+    const Layer& L = h->layers[rb.convs[e]];
+    p.dil[e] = L.dil;
+    flop += 2.0 * L.C_out * L.C_in * L.k * (double)Lt * B;
+  }
+  p.halo = rb.halo;
+  p.W = rb.W;
   p.mrf = mrf;
   p.mrf_mode = mrf_mode;
   p.mrf_div = mrf_div;
-  p.n_chunks = L1.n_chunks;
   p.dbg = h->dbg_flags;
-  const int n_tiles = (int)((Lt + hfg::pair_tile_cols(L1.KT) - 1) / hfg::pair_tile_cols(L1.KT));
-  const double flop = 2.0 * 2.0 * L1.C_out * L1.C_in * L1.k * (double)Lt * B;
-  double bytes = 4.0 * B * Lt * (L1.C_in + L2.C_out) + 2 * 4.0 * L1.C_out * L1.C_in * L1.k;
-  if (mrf && (mrf_mode & 1)) bytes += 4.0 * B * Lt * L2.C_out;
+  const double bytes = 4.0 * B * Lt * C * ((mrf_mode & 1) ? 3 : 2) + 4.0 * (double)rb.w_len;
   const char* name = nullptr;
   ln.begin(flop, bytes);
-  hipError_t e = hfg::launch_pair_bf16x3(L1.tile, L1.KT, p, n_tiles, (int)B, ln.stream, &name);
+  hipError_t e = hfg::launch_resblock_bf16x3(C, rb.waves_n, rb.kt, p, (int)B, ln.stream, &name);
   ln.end(name);
   if (e != hipSuccess)
-    return fail(HFG_EIO, "launch pair %s: %s", L1.mod.c_str(), hipGetErrorString(e));
+    return fail(HFG_EIO, "launch resblock %s: %s", L0.mod.c_str(), hipGetErrorString(e));
   return HFG_OK;
 }
 
@@ -663,28 +742,21 @@ int forward_impl(hfg_handle* h, const float* mel, int64_t B, int64_t T, const hf
     rc = run_ups(h, ln, h->layers[st.conv_ups], cur, B, Lin, L, X, lens_at(i), lens_at(i + 1));
     if (rc) return rc;
     // MRF (models/hifigan.py:116-131) of ResBlocks (:72-86)
+    if (st.fused) {
+      for (int j = 0; j < c.n_res; ++j) {
+        const int mode = (j > 0 ? 1 : 0) | (j == c.n_res - 1 ? 2 : 0);
+        rc = run_resblock(h, ln, st.rbs[j], X, B, L, MRF, mode, (float)c.n_res, lens_at(i + 1));
+        if (rc) return rc;
+      }
+      cur = MRF;
+      continue;
+    }
     int idx = 0;
     for (int j = 0; j < c.n_res; ++j) {
-      const float* psrc = X;  // fused path: ping-pong R / Tb (a pair may not write its input)
       for (int m = 0; m < c.n_dil[j]; ++m, ++idx) {
         const float* src = (m == 0) ? X : R;
         const Layer& L1 = h->layers[st.conv1[idx]];
         const Layer& L2 = h->layers[st.conv2[idx]];
-        if (h->use_pair && L1.prec == 1 && L2.prec == 1 && L2.KT == L1.KT && L2.dil == 1 &&
-            L2.tile == L1.tile && hfg::pair_supported(L1.tile, L1.m_tiles, L1.KT, L1.dil)) {
-          const bool last = (m == c.n_dil[j] - 1);
-          if (!last) {
-            float* dst = (m % 2 == 0) ? R : Tb;
-            rc = run_pair(h, ln, L1, L2, psrc, B, L, dst, nullptr, 0, 1.f, lens_at(i + 1));
-            psrc = dst;
-          } else {
-            int mode = (j > 0 ? 1 : 0) | (j == c.n_res - 1 ? 2 : 0);
-            rc = run_pair(h, ln, L1, L2, psrc, B, L, nullptr, MRF, mode, (float)c.n_res,
-                          lens_at(i + 1));
-          }
-          if (rc) return rc;
-          continue;
-        }
         // xt = lrelu(conv1(lrelu(x)))
         rc = run_conv(h, ln, L1, src, B, L, Tb, true, true, nullptr, nullptr, 0, 1.f,
                       lens_at(i + 1));
@@ -750,7 +822,11 @@ int hfg_create(const hfg_config* cfg, int device, hfg_handle** out) {
     const int v = atoi(bt);
     if (v == 0 || v == 3) h->big_tile = v;
   }
-  if (const char* pe = getenv("HFG_PAIR")) h->use_pair = atoi(pe) != 0;
+  if (const char* fe = getenv("HFG_FUSED_RB")) h->use_fused_rb = atoi(fe) != 0;
+  if (const char* we = getenv("HFG_RB_WN32")) {
+    const int v = atoi(we);
+    if (v == 4 || v == 8) h->rb_waves_n32 = v;
+  }
   build_layers(h);
   *out = h;
   return HFG_OK;
@@ -1005,6 +1081,34 @@ int hfg_debug_packed_layer(hfg_handle* h, const char* mod, float* out, size_t ca
     return HFG_OK;
   }
   return fail(HFG_EINVAL, "unknown layer '%s'", mod);
+}
+
+int hfg_debug_packed_resblock(hfg_handle* h, int stage, int j, float* out, size_t cap,
+                              int64_t* info) {
+  if (!h || !info) return fail(HFG_EINVAL, "NULL argument");
+  if (stage < 0 || stage >= (int)h->stages.size()) return fail(HFG_EINVAL, "stage out of range");
+  const Stage& st = h->stages[stage];
+  for (int i = 0; i < 8; ++i) info[i] = 0;
+  if (!st.fused) return HFG_OK;
+  if (j < 0 || j >= (int)st.rbs.size()) return fail(HFG_EINVAL, "resblock out of range");
+  const RbFused& rb = st.rbs[j];
+  info[0] = 1;
+  info[1] = h->layers[rb.convs[0]].C_out;
+  info[2] = rb.kt;
+  info[3] = (int64_t)rb.convs.size();
+  info[4] = rb.halo;
+  info[5] = rb.W;
+  info[6] = (int64_t)rb.w_len;
+  info[7] = (int64_t)rb.b_len;
+  if (!out) return HFG_OK;
+  if (h->dirty) {
+    int rc = do_commit(h);
+    if (rc) return rc;
+  }
+  if (cap < rb.w_len + rb.b_len) return fail(HFG_EINVAL, "output buffer too small");
+  memcpy(out, h->packed_host.data() + rb.w_off, sizeof(float) * rb.w_len);
+  memcpy(out + rb.w_len, h->packed_host.data() + rb.b_off, sizeof(float) * rb.b_len);
+  return HFG_OK;
 }
 
 }  // extern "C"

@@ -36,8 +36,6 @@ struct ConvParams {
   float mrf_div;
   int ups_s, ups_p, L_out;  // UPS store mapping
   int n_chunks;      // ceil(C_in / CK)
-  const float* w2;   // ResBlock pair kernel: conv2's packed weights / bias (conv1 in w, bias)
-  const float* bias2;
   int dbg;           // ablation flags (HFG_DEBUG_FLAGS; 0 in production; wrong results when
                      // set), bf16x3 kernel: bit0 skip input restaging after the first
                      // chunk, bit2 no per-chunk barrier, bit3 no epilogue
@@ -110,18 +108,33 @@ size_t bf16x3_lds_bytes(int tile, int kt, int dil);
 hipError_t launch_conv_bf16x3(int tile, int kt, bool ups, const ConvParams& p, int n_tiles,
                               int m_tiles, int batch, hipStream_t stream, const char** name);
 
-// ---- fused ResBlock dilation step (conv_pair_bf16x3.hip) ----
-// out = x + conv2(lrelu(conv1(lrelu(x)))) (models/hifigan.py:79-85) in one launch for
-// C in {32, 64}: conv1's output never leaves LDS.  Uses the bf16x3 packing of tile 1
-// (C = 64) or tile 2 (C = 32); a block computes pair_tile_cols(tile, k) outputs.
-constexpr int kPairCols = 128;  // GEMM columns per phase (4 waves x 32)
-inline bool pair_supported(int tile, int m_tiles, int kt, int dil) {
-  return (tile == 1 || tile == 2) && m_tiles == 1 && kt >= 1 && kt <= 16 && dil <= kMaxDil;
-}
-inline int pair_tile_cols(int kt) { return kPairCols - (kt - 1); }
-size_t pair_lds_bytes(int tile, int kt, int dil);
-hipError_t launch_pair_bf16x3(int tile, int kt, const ConvParams& p, int n_tiles, int batch,
-                              hipStream_t stream, const char** name);
+// ---- whole ResBlock per launch (resblock_bf16x3.hip) ----
+// All 2*n_dil convs of one ResBlock of a C in {32, 64} stage on a window of
+// kRbColsPerWave * waves_n columns; x in registers, the conv operand in LDS.
+constexpr int kRbColsPerWave = 128;
+constexpr int kRbMaxConv = 16;
+constexpr int kRbMarg = 48;  // spare operand rows per side: every conv's (k-1)/2*dil <= this
+struct RbParams {
+  const float* x;        // stage input [B][C][L]
+  int64_t bs;            // batch stride of x and mrf (C * L)
+  int L;                 // row length
+  const int32_t* len;    // per-item valid length (device, [B]) or null = L
+  const __bf16* w;       // packed A stream [wave_m][conv][group][tap][plane][lane][8]
+  int w_bytes;           // its size (buffer descriptor range)
+  const float* bias;     // [conv][C]
+  int n_conv;            // 2 * n_dil, order conv1_0, conv2_0, conv1_1, ...
+  int dil[kRbMaxConv];   // dilation of each conv
+  int halo, W;           // receptive-field radius, output columns per block
+  float* mrf;            // MRF accumulator [B][C][L]
+  int mrf_mode;          // bit0: add the existing value, bit1: divide by mrf_div
+  float mrf_div;
+  int dbg;               // ablations (HFG_DEBUG_FLAGS, wrong results when set): bit4 no MRF
+                         // epilogue, bit5 no x loads, bit6 no operand writes
+};
+bool rb_supported(int C, int kt, int waves_n);
+size_t rb_lds_bytes(int C, int waves_n, int n_conv);
+hipError_t launch_resblock_bf16x3(int C, int waves_n, int kt, const RbParams& p, int batch,
+                                  hipStream_t stream, const char** name);
 
 // Launch the conv kernel for (tile, taps, ups).  Returns a hipError_t and,
 // via *name, the kernel's template-instance name (as rocprofv3 prints it).

@@ -1,0 +1,344 @@
+// resblock_bf16x3.hip — one whole ResBlock per launch (bf16x3 MFMA), for the
+// narrow stages (C in {32, 64}) where a layer-per-launch schedule is bound by HBM
+// round trips, not by the matrix cores:
+//
+//   for m in dilations:  x = x + conv2_m(lrelu(conv1_m(lrelu(x))))   models/hifigan.py:79-85
+//   mrf = (mrf + x) [/ n_res]                                         models/hifigan.py:125-131
+//
+// A block owns a window of NWIN time columns [ws, ws + NWIN) of one utterance and
+// writes the centre [ws + halo, ws + halo + W), W = NWIN - 2*halo, where halo is the
+// ResBlock's receptive-field radius (sum over its convs of (k-1)/2 * dilation).  All
+// 2*n_dil convs run on the whole window; columns within a conv's radius of the window
+// edge become garbage and the garbage front moves inwards by exactly that radius, so
+// the centre is exact.  Columns outside [0, len) are re-zeroed after every conv — the
+// reference's zero padding of each conv input.
+//
+// State: the residual stream x lives in registers (fp32, MFMA accumulator layout:
+// every wave owns 32 rows x 128 columns of the window for the whole block), the
+// current conv's B operand lives in LDS as bf16 hi/lo planes [group][plane][col][16]
+// (one buffer, rewritten in place after a barrier).  The A operand (weights) is
+// streamed from global memory (L2/L1-resident: every block reads the same stream)
+// straight into registers two k-steps ahead; it is packed per wave row-block as
+// [wave_m][conv][group][tap][plane][lane][8] so each k-step is 2 x 1 KB coalesced.
+//
+// Channel order inside a 16-channel group is permuted (slot 8h+e <-> channel
+// 4h + (e&3) + 8(e>>2)) so that the rows one lane holds in the accumulator layout are
+// exactly the 8 slots it reads as a B fragment: the epilogue writes the next conv's
+// operand with one ds_write_b128 per plane and group.  The weight packer applies the
+// same permutation to the K index.
+//
+// HBM traffic per ResBlock: x once (+ halo), MRF read-modify-write once, vs 5 tensor
+// passes per dilation for the layer-per-launch schedule.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+
+#include "bf16x3_common.h"
+#include "kernels.h"
+
+namespace hfg {
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef float floatx2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+
+template <int KT, int WAVES_M, int WAVES_N>
+__global__ void __launch_bounds__(64 * WAVES_M * WAVES_N, 2)  // 2 waves/SIMD: <= 256 VGPRs
+resblock_bf16x3(const RbParams p) {
+  constexpr int NW = WAVES_M * WAVES_N;
+  constexpr int NT = 64 * NW;
+  constexpr int C = 32 * WAVES_M;
+  constexpr int NG = C / 16;               // 16-channel groups
+  constexpr int WN = 4;                    // 32-column MFMA tiles per wave
+  constexpr int NWIN = 32 * WN * WAVES_N;  // window columns
+  constexpr int STEPS = NG * KT;           // MFMA k-steps per conv
+  static_assert(STEPS % 2 == 0, "two-deep A register ring needs an even step count");
+  // operand rows: the window plus kRbMarg spare rows on each side, read (never written)
+  // by the taps of edge columns; their contents only reach garbage columns
+  constexpr int ROWS = NWIN + 2 * kRbMarg;
+  constexpr int PS = ROWS * 16;            // bytes per plane: [row][8 bf16]
+  constexpr int HPS = 2 * PS;              // half-group (slots 0-7 | 8-15): hi, lo planes
+  constexpr int GS = 2 * HPS;              // 16-channel group
+  constexpr int ASTEP = 2 * 64 * 16;       // bytes per k-step of one wave row-block (hi, lo)
+
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  float* const bias_s = reinterpret_cast<float*>(lds + NG * GS);
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wave_m = wave % WAVES_M;
+  const int wave_n = wave / WAVES_M;
+  const int half = lane >> 5;
+  const int col = lane & 31;
+  const int b = blockIdx.y;
+  const int len_b = p.len ? min(p.len[b], p.L) : p.L;
+  const int t0 = blockIdx.x * p.W;
+  if (t0 >= len_b) return;  // whole block past this utterance's end (block-uniform)
+  const int ws = t0 - p.halo;
+  const int cbase = wave_n * 32 * WN;      // first window column of this wave
+  const int row0 = wave_m * 32;
+  const int n_conv = p.n_conv;
+  const int QT = n_conv * STEPS;
+  const int dbg = p.dbg;
+  auto rrow = [&](int r) { return (r & 3) + 8 * (r >> 2) + 4 * half; };
+
+  for (int i = tid; i < n_conv * C; i += NT) bias_s[i] = p.bias[i];
+
+  bool vk[WN];
+  bool wave_valid = true;  // every column of this wave inside [0, len)
+#pragma unroll
+  for (int k = 0; k < WN; ++k) {
+    vk[k] = (unsigned)(ws + cbase + 32 * k + col) < (unsigned)len_b;
+    wave_valid = wave_valid && (unsigned)(ws + cbase + 32 * k) < (unsigned)len_b &&
+                 (unsigned)(ws + cbase + 32 * k + 31) < (unsigned)len_b;
+  }
+
+  // ---- A stream (buffer loads: SGPR descriptor + scalar step offset, no address VALU) ----
+  const __amdgpu_buffer_rsrc_t wrs =
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.w, 0, p.w_bytes, 0x00020000);
+  const int a_base = wave_m * QT * ASTEP;
+  const int a_lane = lane * 16;
+  bf16x8 ra_h[2], ra_l[2];
+  auto load_a = [&](int slot, int q) {
+    const int so = a_base + min(q, QT - 1) * ASTEP;
+    ra_h[slot] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(wrs, a_lane, so, 0));
+    ra_l[slot] =
+        __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(wrs, a_lane + 1024, so, 0));
+  };
+  load_a(0, 0);
+  load_a(1, 1);
+
+  // ---- residual stream x: window -> registers (zero outside [0, len)) ----
+  floatx16 xcur[WN];
+  {
+    const float* __restrict__ xb = p.x + (int64_t)b * p.bs;
+#pragma unroll
+    for (int k = 0; k < WN; ++k) {
+      const int ta = ws + cbase + 32 * k + col;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const unsigned off = vk[k] ? (unsigned)((row0 + rrow(r)) * p.L + ta) : 0u;
+        xcur[k][r] = (dbg & 32) ? 0.f : xb[off];
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < WN; ++k)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) xcur[k][r] = vk[k] ? xcur[k][r] : 0.f;
+  }
+
+  // lane's byte address of window column (cbase + col) in its half-group's hi plane
+  const int vb = half * HPS + (cbase + col + kRbMarg) * 16;
+
+  // B operand of the next conv: lrelu(v), zero outside [0, len), split hi/lo -> LDS.
+  // The 8 accumulator rows a lane holds per 16-channel group are exactly the 8 slots
+  // (one 16-B row of its half-group) it reads as a B fragment.
+  auto write_operand = [&](const floatx16 (&v)[WN]) {
+    if (dbg & 64) return;
+#pragma unroll
+    for (int k = 0; k < WN; ++k) {
+#pragma unroll
+      for (int gg = 0; gg < 2; ++gg) {
+        bf16x8 h, l;
+#pragma unroll
+        for (int e = 0; e < 8; e += 2) {
+          floatx2 a;
+          a[0] = v[k][gg * 8 + e];
+          a[1] = v[k][gg * 8 + e + 1];
+          a[0] = lrelu3(a[0]);
+          a[1] = lrelu3(a[1]);
+          if (!wave_valid) {
+            a[0] = vk[k] ? a[0] : 0.f;
+            a[1] = vk[k] ? a[1] : 0.f;
+          }
+          const bf16x2 hh = __builtin_convertvector(a, bf16x2);
+          const floatx2 hf = __builtin_convertvector(hh, floatx2);
+          const bf16x2 ll = __builtin_convertvector(a - hf, bf16x2);
+          h[e] = hh[0];
+          h[e + 1] = hh[1];
+          l[e] = ll[0];
+          l[e + 1] = ll[1];
+        }
+        char* dst = lds + (wave_m * 2 + gg) * GS + vb + k * 512;
+        *reinterpret_cast<bf16x8*>(dst) = h;
+        *reinterpret_cast<bf16x8*>(dst + PS) = l;
+      }
+    }
+  };
+  write_operand(xcur);
+  lds_barrier();
+
+  // conv cv over the whole window: acc = bias + W_cv * operand (one LDS barrier at the
+  // end: every wave has read the operand, which the caller then overwrites in place)
+  floatx16 acc[WN];
+  auto run_conv = [&](int cv) {
+    const int d = p.dil[cv];
+    const int pad = (KT - 1) / 2 * d;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const float bv = bias_s[cv * C + row0 + rrow(r)];
+#pragma unroll
+      for (int k = 0; k < WN; ++k) acc[k][r] = bv;
+    }
+    bf16x8 bh[2][WN], bl[2][WN];
+    // step s = (group g, tap j): rows shifted by j*d - pad, one VALU add per step,
+    // tiles / planes by immediate offsets
+    auto load_b = [&](int buf, int s) {
+      const int g = s / KT, j = s - (s / KT) * KT;
+      const char* src = lds + vb + (g * GS + (j * d - pad) * 16);
+#pragma unroll
+      for (int k = 0; k < WN; ++k) {
+        bh[buf][k] = *reinterpret_cast<const bf16x8*>(src + k * 512);
+        bl[buf][k] = *reinterpret_cast<const bf16x8*>(src + k * 512 + PS);
+      }
+    };
+    const int qb = cv * STEPS;
+    load_b(0, 0);
+    // software pipeline: B fragments one step ahead (interleaved with this step's
+    // MFMAs), A fragments two steps ahead
+#pragma unroll
+    for (int s = 0; s < STEPS; ++s) {
+      const int cur = s & 1;
+      if (s + 1 < STEPS) load_b(cur ^ 1, s + 1);
+#pragma unroll
+      for (int k = 0; k < WN; ++k) {
+        acc[k] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ra_l[cur], bh[cur][k], acc[k], 0, 0, 0);
+        acc[k] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ra_h[cur], bl[cur][k], acc[k], 0, 0, 0);
+        acc[k] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ra_h[cur], bh[cur][k], acc[k], 0, 0, 0);
+      }
+      load_a(cur, qb + s + 2);
+      if (s + 1 < STEPS) {
+#pragma unroll
+        for (int i = 0; i < 2 * WN; ++i) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // 1 MFMA
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // 1 DS read
+        }
+      }
+      __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);    // 2 MFMA
+      __builtin_amdgcn_sched_group_barrier(0x020, 2, 0);    // A loads
+      __builtin_amdgcn_sched_group_barrier(0x008, 3 * WN, 0);  // rest of the MFMAs
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    lds_barrier();
+  };
+
+  // dilation pairs: xt = lrelu(conv1(lrelu(x)) + b1); x = x + (conv2(xt) + b2)
+  for (int cv = 0; cv < n_conv; cv += 2) {
+    run_conv(cv);
+    write_operand(acc);
+    lds_barrier();
+    run_conv(cv + 1);
+#pragma unroll
+    for (int k = 0; k < WN; ++k)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) xcur[k][r] = xcur[k][r] + acc[k][r];
+    if (cv + 2 < n_conv) {
+      write_operand(xcur);
+      lds_barrier();
+    }
+  }
+
+  // ---- MRF: (mrf + x) [/ n_res] on the window centre ----
+  if (dbg & 16) {  // ablation: no MRF epilogue
+    if (xcur[0][0] == 1.2345e-30f) p.mrf[0] = xcur[WN - 1][15];
+    return;
+  }
+  float* __restrict__ mb = p.mrf + (int64_t)b * p.bs;
+  const bool add = p.mrf_mode & 1;
+  const bool div = p.mrf_mode & 2;
+#pragma unroll
+  for (int k = 0; k < WN; ++k) {
+    const int c = cbase + 32 * k + col;
+    const bool ok = vk[k] && c >= p.halo && c < p.halo + p.W;
+    const int ta = ws + c;
+    unsigned off[16];
+    float v[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      off[r] = ok ? (unsigned)((row0 + rrow(r)) * p.L + ta) : 0u;
+      v[r] = xcur[k][r];
+    }
+    if (add) {
+      float mv[16];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) mv[r] = mb[off[r]];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) v[r] = mv[r] + v[r];
+    }
+    if (div) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) v[r] = v[r] / p.mrf_div;
+    }
+    if (ok) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) mb[off[r]] = v[r];
+    }
+  }
+}
+
+namespace {
+
+typedef void (*RbFn)(const RbParams);
+
+struct EntryRb {
+  int kt, waves_m, waves_n;
+  RbFn fn;
+  bool attr;
+  char name[64];
+};
+
+#define HFGRB_ENTRY(KT, WMS, WNS) \
+  { KT, WMS, WNS, resblock_bf16x3<KT, WMS, WNS>, false, {0} }
+#define HFGRB_KTS(WMS, WNS)                                                             \
+  HFGRB_ENTRY(3, WMS, WNS), HFGRB_ENTRY(5, WMS, WNS), HFGRB_ENTRY(7, WMS, WNS), \
+      HFGRB_ENTRY(11, WMS, WNS)
+
+EntryRb g_entriesRb[] = {HFGRB_KTS(2, 4), HFGRB_KTS(1, 8), HFGRB_KTS(1, 4)};
+
+}  // namespace
+
+bool rb_supported(int C, int kt, int waves_n) {
+  if (kt != 3 && kt != 5 && kt != 7 && kt != 11) return false;
+  const int wm = C / 32;
+  if (C % 32 != 0) return false;
+  for (auto& e : g_entriesRb)
+    if (e.kt == kt && e.waves_m == wm && e.waves_n == waves_n) return true;
+  return false;
+}
+
+size_t rb_lds_bytes(int C, int waves_n, int n_conv) {
+  const size_t rows = (size_t)kRbColsPerWave * waves_n + 2 * kRbMarg;
+  return (size_t)C * rows * 4 + sizeof(float) * (size_t)n_conv * C;
+}
+
+hipError_t launch_resblock_bf16x3(int C, int waves_n, int kt, const RbParams& p, int batch,
+                                  hipStream_t stream, const char** name) {
+  const int wm = C / 32;
+  EntryRb* e = nullptr;
+  for (auto& cand : g_entriesRb)
+    if (cand.kt == kt && cand.waves_m == wm && cand.waves_n == waves_n) e = &cand;
+  if (!e || C % 32 != 0) return hipErrorInvalidValue;
+  const int nwin = kRbColsPerWave * waves_n;
+  if (p.n_conv < 2 || p.n_conv > kRbMaxConv || (p.n_conv & 1)) return hipErrorInvalidValue;
+  if (p.W <= 0 || p.halo < 0 || p.W + 2 * p.halo > nwin) return hipErrorInvalidValue;
+  for (int i = 0; i < p.n_conv; ++i)
+    if (p.dil[i] < 1 || (kt - 1) / 2 * p.dil[i] > kRbMarg) return hipErrorInvalidValue;
+  if (!e->name[0])
+    snprintf(e->name, sizeof(e->name), "resblock_bf16x3<%d, %d, %d>", e->kt, e->waves_m,
+             e->waves_n);
+  const size_t lds = rb_lds_bytes(C, waves_n, p.n_conv);
+  if (lds > 160 * 1024) return hipErrorInvalidValue;
+  if (!e->attr) {
+    hipError_t err = hipFuncSetAttribute(reinterpret_cast<const void*>(e->fn),
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    if (err != hipSuccess) return err;
+    e->attr = true;
+  }
+  if (name) *name = e->name;
+  const int n_tiles = (p.L + p.W - 1) / p.W;
+  e->fn<<<dim3(n_tiles, batch), dim3(64 * wm * waves_n), lds, stream>>>(p);
+  return hipGetLastError();
+}
+
+}  // namespace hfg
