@@ -95,11 +95,13 @@ def test_golden_fixture_bf16x3(pkg, golden_index, name):
     assert rel < 1e-3, rel
 
 
-@pytest.mark.parametrize("big_tile,fused,wn32", [("0", "1", "8"), ("3", "1", "4"), ("3", "0", "8")])
+@pytest.mark.parametrize("big_tile,fused,wn32",
+                         [("4", "1", "4"), ("4", "0", "8"), ("3", "1", "4"), ("0", "1", "8")])
 @pytest.mark.parametrize("preset,B,T", [("v1", 2, 300), ("v2star", 2, 200)])
 def test_bf16x3_vs_oracle_longer(pkg, preset, B, T, big_tile, fused, wn32, monkeypatch):
     """Random weights/mel vs the oracle, with each tile choice for the M >= 128 layers
-    (HFG_BF16X3_BIGTILE: 0 = 128x256 8-wave, 3 = 128x256 4-wave) and with the
+    (HFG_BF16X3_BIGTILE: 0 = 128x256 8-wave, 3 = 128x256 4-wave, 4 = warp-specialized
+    128x256, default) and with the
     whole-ResBlock kernel for C in {32, 64} on (HFG_FUSED_RB=1, default; C = 32 window
     512 or 1024 columns) or off (layer per launch)."""
     from oracle import config as C, prng

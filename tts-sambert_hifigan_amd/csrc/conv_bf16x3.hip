@@ -265,25 +265,54 @@ conv1d_bf16x3(const ConvParams p) {
 
   // ---- epilogue (same contract as conv1d_mfma_f32) ----
   if constexpr (UPS) {
-    // polyphase scatter: GEMM row m = co*s + r lands at t = n*s + r - p
+    // polyphase scatter: GEMM row m = co*s + r lands at t = n*s + r - p.  A lane holds
+    // rows 4q..4q+3 (q = r>>2 block of its half): with s % 4 == 0 and p % 4 == 0 those
+    // are 4 consecutive phases of one co, i.e. 4 consecutive output samples at a 16-B
+    // aligned t: one float4 store instead of four scattered dword stores.
+    const int s_ = p.ups_s, p_ = p.ups_p;
+    const bool vec4 = (s_ & 3) == 0 && (p_ & 3) == 0 && (p.L_out & 3) == 0;
+    float* __restrict__ yb = p.y + (int64_t)b * p.y_bs;
 #pragma unroll
     for (int i = 0; i < WM; ++i) {
+      const int rb = mt * MT + wave_m * 32 * WM + i * 32 + 4 * half;  // row of r = 0
       float bv[16];
 #pragma unroll
-      for (int r = 0; r < 16; ++r)
-        bv[r] = p.bias[mt * MT + wave_m * 32 * WM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * half];
+      for (int r = 0; r < 16; ++r) bv[r] = p.bias[rb + (r & 3) + 8 * (r >> 2)];
 #pragma unroll
       for (int k = 0; k < WN; ++k) {
         const int n = n0 + wave_n * 32 * WN + k * 32 + col;
         if (n >= N_b) continue;
+        if (vec4) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int row = rb + 8 * q;
+            if (row >= p.M) continue;
+            const int co = row / s_;
+            const int t = n * s_ + (row - co * s_) - p_;
+            float4 v;
+            v.x = acc[i][k][4 * q + 0] + bv[4 * q + 0];
+            v.y = acc[i][k][4 * q + 1] + bv[4 * q + 1];
+            v.z = acc[i][k][4 * q + 2] + bv[4 * q + 2];
+            v.w = acc[i][k][4 * q + 3] + bv[4 * q + 3];
+            float* dst = yb + (int64_t)co * p.L_out + t;
+            if (t >= 0 && t + 3 < L_out_b) {
+              *reinterpret_cast<float4*>(dst) = v;
+            } else {
+              if (t + 0 >= 0 && t + 0 < L_out_b) dst[0] = v.x;
+              if (t + 1 >= 0 && t + 1 < L_out_b) dst[1] = v.y;
+              if (t + 2 >= 0 && t + 2 < L_out_b) dst[2] = v.z;
+              if (t + 3 >= 0 && t + 3 < L_out_b) dst[3] = v.w;
+            }
+          }
+          continue;
+        }
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const int row = mt * MT + wave_m * 32 * WM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
+          const int row = rb + (r & 3) + 8 * (r >> 2);
           if (row >= p.M) continue;
-          const int co = row / p.ups_s;
-          const int t = n * p.ups_s + (row - co * p.ups_s) - p.ups_p;
-          if (t >= 0 && t < L_out_b)
-            p.y[(int64_t)b * p.y_bs + (int64_t)co * p.L_out + t] = acc[i][k][r] + bv[r];
+          const int co = row / s_;
+          const int t = n * s_ + (row - co * s_) - p_;
+          if (t >= 0 && t < L_out_b) yb[(int64_t)co * p.L_out + t] = acc[i][k][r] + bv[r];
         }
       }
     }

@@ -75,6 +75,7 @@ struct ProfRec {
 // [wave_m][conv][group][tap][plane][lane][8] and biases [conv][C] in the packed buffer.
 struct RbFused {
   std::vector<int> convs;     // layer indices in execution order conv1_0, conv2_0, conv1_1, ...
+  bool fused = false;         // this ResBlock runs as one resblock_bf16x3 launch
   int kt = 0, halo = 0, W = 0, waves_n = 0;
   size_t w_off = 0, w_len = 0, b_off = 0, b_len = 0;  // in floats
 };
@@ -83,8 +84,7 @@ struct Stage {
   int conv_ups;               // index of the ups layer
   std::vector<int> conv1;     // [j*n_dil + m]
   std::vector<int> conv2;
-  bool fused = false;         // MRF run as one resblock_bf16x3 launch per ResBlock
-  std::vector<RbFused> rbs;
+  std::vector<RbFused> rbs;   // per ResBlock: whole-block launch or layer by layer
 };
 
 }  // namespace
@@ -105,7 +105,8 @@ struct hfg_handle {
   void* ws = nullptr;
   size_t ws_bytes = 0;
   bool profiling = false;
-  int big_tile = 3;   // bf16x3 tile for M >= 128 (HFG_BF16X3_BIGTILE env: 0 or 3)
+  int big_tile = 3;  // bf16x3 tile for M >= 128 (HFG_BF16X3_BIGTILE env: 0, 3 or 4 =
+                     // warp-specialized conv_ws_bf16x3, measured ~3-15% slower than 3 on r01)
   bool use_fused_rb = true;  // whole-ResBlock kernel for C in {32, 64} (HFG_FUSED_RB=0 disables)
   int rb_waves_n32 = 4;      // window of the C = 32 ResBlock kernel: 128 * this columns
                              // (HFG_RB_WN32: 4 or 8)
@@ -234,9 +235,25 @@ void build_layers(hfg_handle* h) {
       continue;
     }
     if (h->cfg.dtype == HFG_DTYPE_BF16X3 && (L.kind == L_CONV || L.kind == L_UPS) &&
+        h->big_tile == hfg::kWsTile && hfg::ws_supported(L.KT, L.kind == L_UPS, L.M, L.dil)) {
+      // warp-specialized path: A stream [m_tile][wave_m][group][tap][plane][lane][8]
+      L.prec = 1;
+      L.tile = hfg::kWsTile;
+      L.CK = hfg::kBf16x3Ck;
+      L.m_tiles = L.M / hfg::kWsMT;
+      L.n_chunks = (L.C_in + 15) / 16;
+      L.w_off = off;
+      L.w_len = (size_t)L.m_tiles * 4 * L.n_chunks * L.KT * 1024 / 2;  // bf16 pairs as floats
+      off += (L.w_len + 63) & ~(size_t)63;
+      L.b_off = off;
+      L.b_len = (size_t)L.m_tiles * hfg::kWsMT;
+      off += (L.b_len + 63) & ~(size_t)63;
+      continue;
+    }
+    if (h->cfg.dtype == HFG_DTYPE_BF16X3 && (L.kind == L_CONV || L.kind == L_UPS) &&
         hfg::bf16x3_tile_for_rows(L.M) >= 0) {
       // split-precision path: chunk = 16 channels x TPC taps
-      L.tile = hfg::bf16x3_tile_for_rows(L.M, h->big_tile);
+      L.tile = hfg::bf16x3_tile_for_rows(L.M, h->big_tile == hfg::kWsTile ? 3 : h->big_tile);
       const hfg::Bf16x3Cfg& t3 = hfg::kBf16x3Tiles[L.tile];
       L.prec = 1;
       L.CK = hfg::kBf16x3Ck;
@@ -264,44 +281,42 @@ void build_layers(hfg_handle* h) {
     L.b_len = (size_t)L.m_tiles * t.MT();
     off += (L.b_len + 63) & ~(size_t)63;
   }
-  // whole-ResBlock launches for the narrow stages (bf16x3 only)
+  // whole-ResBlock launches (bf16x3 only): every ResBlock of the C in {32, 64} stages, and
+  // those of C = 128 whose receptive field costs <= 15% recomputation (k = 3 in V1)
   for (int i = 0; i < c.n_up; ++i) {
     Stage& st = h->stages[i];
     const int C = c.c0 >> (i + 1);
-    if (h->cfg.dtype != HFG_DTYPE_BF16X3 || !h->use_fused_rb || (C != 32 && C != 64)) continue;
-    const int waves_n = C == 64 ? 4 : h->rb_waves_n32;
+    st.rbs.assign(c.n_res, RbFused{});
+    if (h->cfg.dtype != HFG_DTYPE_BF16X3 || !h->use_fused_rb || (C != 32 && C != 64 && C != 128))
+      continue;
+    const int waves_n = C == 128 ? 2 : C == 64 ? 4 : h->rb_waves_n32;
     const int nwin = hfg::kRbColsPerWave * waves_n;
-    std::vector<RbFused> rbs;
-    bool ok = true;
     int idx = 0;
-    for (int j = 0; j < c.n_res && ok; ++j) {
+    for (int j = 0; j < c.n_res; ++j) {
       RbFused rb;
       rb.kt = c.res_kernels[j];
       rb.waves_n = waves_n;
-      if (rb.kt % 2 == 0 || !hfg::rb_supported(C, rb.kt, waves_n) ||
-          2 * c.n_dil[j] > hfg::kRbMaxConv) {
-        ok = false;
-        break;
-      }
+      bool ok = rb.kt % 2 == 1 && hfg::rb_supported(C, rb.kt, waves_n) &&
+                2 * c.n_dil[j] <= hfg::kRbMaxConv;
       for (int m = 0; m < c.n_dil[j]; ++m, ++idx) {
         rb.convs.push_back(st.conv1[idx]);
         rb.convs.push_back(st.conv2[idx]);
         rb.halo += (rb.kt - 1) / 2 * c.dil[j][m] + (rb.kt - 1) / 2;
-        if ((rb.kt - 1) / 2 * c.dil[j][m] > hfg::kRbMarg) ok = false;
+        if ((rb.kt - 1) / 2 * c.dil[j][m] > hfg::rb_marg(C)) ok = false;
       }
       rb.W = nwin - 2 * rb.halo;
       if (rb.W < nwin / 4) ok = false;
+      if (C == 128 && (double)nwin / rb.W > 1.15) ok = false;
+      if (!ok) continue;
+      rb.fused = true;
       rb.w_off = off;
       rb.w_len = (size_t)rb.convs.size() * C * C * rb.kt;  // bf16 hi + lo = one float each
       off += (rb.w_len + 63) & ~(size_t)63;
       rb.b_off = off;
       rb.b_len = rb.convs.size() * (size_t)C;
       off += (rb.b_len + 63) & ~(size_t)63;
-      rbs.push_back(rb);
+      st.rbs[j] = std::move(rb);
     }
-    if (!ok) continue;  // the (unused) offsets stay reserved; harmless
-    st.fused = true;
-    st.rbs = std::move(rbs);
   }
   h->packed_host.assign(off, 0.f);
 }
@@ -348,6 +363,30 @@ inline float bf2f(uint16_t b) {
 //         + lane*8 + e
 //   row = mt*MT + wave_m*32*WM + wm*32 + (lane & 31), ci = g*16 + 8*(lane >> 5) + e,
 //   tap = tg*TPC + jj; plane 0 = bf16(w), plane 1 = bf16(w - hi).
+// A stream of conv_ws_bf16x3 (conv_ws_bf16x3.hip), in bf16 elements:
+//   idx = (((((((mt*2 + wave_m)*n_g + g)*KT + tap)*2 + wm)*2 + plane)*64 + lane)*8 + e
+//   row = mt*128 + wave_m*64 + wm*32 + (lane & 31), ci = g*16 + 8*(lane >> 5) + e.
+template <typename F>
+void pack_ws(const Layer& L, F wt, uint16_t* dst) {
+  const int n_g = L.n_chunks;
+  size_t idx = 0;
+  for (int mt = 0; mt < L.m_tiles; ++mt)
+    for (int wv = 0; wv < 2; ++wv)
+      for (int g = 0; g < n_g; ++g)
+        for (int tap = 0; tap < L.KT; ++tap)
+          for (int wm = 0; wm < 2; ++wm)
+          for (int plane = 0; plane < 2; ++plane)
+            for (int lane = 0; lane < 64; ++lane)
+              for (int e = 0; e < 8; ++e) {
+                const int row = mt * hfg::kWsMT + wv * 64 + wm * 32 + (lane & 31);
+                const int ci = g * 16 + 8 * (lane >> 5) + e;
+                float v = 0.f;
+                if (row < L.M && ci < L.C_in) v = wt(row, ci, tap);
+                const uint16_t hi = f2bf(v);
+                dst[idx++] = plane == 0 ? hi : f2bf(v - bf2f(hi));
+              }
+}
+
 template <typename F>
 void pack_bf16x3(const Layer& L, F wt, uint16_t* dst) {
   const hfg::Bf16x3Cfg& t = hfg::kBf16x3Tiles[L.tile];
@@ -419,6 +458,25 @@ void pack_layer(hfg_handle* h, const Layer& L) {
     bdst[0] = Bp.data[0];
     return;
   }
+  if (L.kind == L_CONV && L.tile == hfg::kWsTile) {
+    const int cin = L.C_in, k = L.k;
+    pack_ws(L, [&](int row, int ci, int j) { return w[((size_t)row * cin + ci) * k + j]; },
+            reinterpret_cast<uint16_t*>(dst));
+    for (size_t m = 0; m < L.b_len; ++m) bdst[m] = m < (size_t)L.M ? Bp.data[m] : 0.f;
+    return;
+  }
+  if (L.kind == L_UPS && L.tile == hfg::kWsTile) {
+    const int s = L.s, Q = L.KT, k = L.k, cout = L.C_out;
+    pack_ws(L,
+            [&](int row, int ci, int jj) {
+              const int co = row / s, r = row % s;
+              const int kidx = r + s * (Q - 1 - jj);
+              return kidx < k ? w[((size_t)ci * cout + co) * k + kidx] : 0.f;
+            },
+            reinterpret_cast<uint16_t*>(dst));
+    for (size_t m = 0; m < L.b_len; ++m) bdst[m] = m < (size_t)L.M ? Bp.data[m / s] : 0.f;
+    return;
+  }
   if (L.kind == L_CONV && L.prec == 1) {
     const int cin = L.C_in, k = L.k;
     pack_bf16x3(L, [&](int row, int ci, int j) { return w[((size_t)row * cin + ci) * k + j]; },
@@ -467,8 +525,8 @@ int do_commit(hfg_handle* h) {
   std::fill(h->packed_host.begin(), h->packed_host.end(), 0.f);
   for (auto& L : h->layers) pack_layer(h, L);
   for (auto& st : h->stages)
-    if (st.fused)
-      for (auto& rb : st.rbs) pack_resblock(h, rb);
+    for (auto& rb : st.rbs)
+      if (rb.fused) pack_resblock(h, rb);
   if (h->device >= 0) {
     DeviceGuard g(h->device);
     if (!g.ok) return fail(HFG_ENODEV, "hipSetDevice(%d) failed", h->device);
@@ -589,7 +647,9 @@ int run_conv(hfg_handle* h, Launcher& ln, const Layer& L, const float* x, int64_
   p.mrf_div = mrf_div;
   p.n_chunks = L.n_chunks;
   p.dbg = h->dbg_flags;
-  const int ntile = L.prec == 1 ? hfg::kBf16x3Tiles[L.tile].NTILE() : kTiles[L.tile].NTILE();
+  const int ntile = L.tile == hfg::kWsTile ? hfg::kWsNT
+                    : L.prec == 1          ? hfg::kBf16x3Tiles[L.tile].NTILE()
+                                           : kTiles[L.tile].NTILE();
   const int n_tiles = (int)((Lt + ntile - 1) / ntile);
   const double flop = 2.0 * L.C_out * L.C_in * L.k * (double)Lt * B;
   double bytes = 4.0 * B * Lt * (L.C_in + L.C_out) + 4.0 * L.C_out * L.C_in * L.k;
@@ -597,7 +657,10 @@ int run_conv(hfg_handle* h, Launcher& ln, const Layer& L, const float* x, int64_
   if (mrf && (mrf_mode & 1)) bytes += 4.0 * B * Lt * L.C_out;
   const char* name = nullptr;
   ln.begin(flop, bytes);
-  hipError_t e = L.prec == 1
+  hipError_t e = L.tile == hfg::kWsTile
+                     ? hfg::launch_conv_ws_bf16x3(L.KT, false, p, n_tiles, L.m_tiles, (int)B,
+                                                  ln.stream, &name)
+                 : L.prec == 1
                      ? hfg::launch_conv_bf16x3(L.tile, L.KT, false, p, n_tiles, L.m_tiles, (int)B,
                                                ln.stream, &name)
                      : hfg::launch_conv((TileId)L.tile, L.KT, false, p, n_tiles, L.m_tiles,
@@ -671,13 +734,18 @@ int run_ups(hfg_handle* h, Launcher& ln, const Layer& L, const float* x, int64_t
   p.L_out = (int)Lout;
   p.n_chunks = L.n_chunks;
   p.dbg = h->dbg_flags;
-  const int ntile = L.prec == 1 ? hfg::kBf16x3Tiles[L.tile].NTILE() : kTiles[L.tile].NTILE();
+  const int ntile = L.tile == hfg::kWsTile ? hfg::kWsNT
+                    : L.prec == 1          ? hfg::kBf16x3Tiles[L.tile].NTILE()
+                                           : kTiles[L.tile].NTILE();
   const int n_tiles = (p.N + ntile - 1) / ntile;
   const double flop = 2.0 * L.C_in * L.C_out * L.k * (double)Lin * B;
   const double bytes = 4.0 * B * (L.C_in * Lin + L.C_out * Lout) + 4.0 * L.C_in * L.C_out * L.k;
   const char* name = nullptr;
   ln.begin(flop, bytes);
-  hipError_t e = L.prec == 1
+  hipError_t e = L.tile == hfg::kWsTile
+                     ? hfg::launch_conv_ws_bf16x3(L.KT, true, p, n_tiles, L.m_tiles, (int)B,
+                                                  ln.stream, &name)
+                 : L.prec == 1
                      ? hfg::launch_conv_bf16x3(L.tile, L.KT, true, p, n_tiles, L.m_tiles, (int)B,
                                                ln.stream, &name)
                      : hfg::launch_conv((TileId)L.tile, L.KT, true, p, n_tiles, L.m_tiles, (int)B,
@@ -742,17 +810,15 @@ int forward_impl(hfg_handle* h, const float* mel, int64_t B, int64_t T, const hf
     rc = run_ups(h, ln, h->layers[st.conv_ups], cur, B, Lin, L, X, lens_at(i), lens_at(i + 1));
     if (rc) return rc;
     // MRF (models/hifigan.py:116-131) of ResBlocks (:72-86)
-    if (st.fused) {
-      for (int j = 0; j < c.n_res; ++j) {
-        const int mode = (j > 0 ? 1 : 0) | (j == c.n_res - 1 ? 2 : 0);
-        rc = run_resblock(h, ln, st.rbs[j], X, B, L, MRF, mode, (float)c.n_res, lens_at(i + 1));
-        if (rc) return rc;
-      }
-      cur = MRF;
-      continue;
-    }
     int idx = 0;
     for (int j = 0; j < c.n_res; ++j) {
+      const int mode = (j > 0 ? 1 : 0) | (j == c.n_res - 1 ? 2 : 0);
+      if (st.rbs[j].fused) {
+        rc = run_resblock(h, ln, st.rbs[j], X, B, L, MRF, mode, (float)c.n_res, lens_at(i + 1));
+        if (rc) return rc;
+        idx += c.n_dil[j];
+        continue;
+      }
       for (int m = 0; m < c.n_dil[j]; ++m, ++idx) {
         const float* src = (m == 0) ? X : R;
         const Layer& L1 = h->layers[st.conv1[idx]];
@@ -767,7 +833,6 @@ int forward_impl(hfg_handle* h, const float* mel, int64_t B, int64_t T, const hf
           rc = run_conv(h, ln, L2, Tb, B, L, R, false, false, src, nullptr, 0, 1.f,
                         lens_at(i + 1));
         } else {
-          int mode = (j > 0 ? 1 : 0) | (j == c.n_res - 1 ? 2 : 0);
           rc = run_conv(h, ln, L2, Tb, B, L, nullptr, false, false, src, MRF, mode,
                         (float)c.n_res, lens_at(i + 1));
         }
@@ -820,7 +885,7 @@ int hfg_create(const hfg_config* cfg, int device, hfg_handle** out) {
   if (const char* dbg = getenv("HFG_DEBUG_FLAGS")) h->dbg_flags = atoi(dbg);
   if (const char* bt = getenv("HFG_BF16X3_BIGTILE")) {
     const int v = atoi(bt);
-    if (v == 0 || v == 3) h->big_tile = v;
+    if (v == 0 || v == 3 || v == hfg::kWsTile) h->big_tile = v;
   }
   if (const char* fe = getenv("HFG_FUSED_RB")) h->use_fused_rb = atoi(fe) != 0;
   if (const char* we = getenv("HFG_RB_WN32")) {
@@ -1067,6 +1132,7 @@ int hfg_debug_packed_layer(hfg_handle* h, const char* mod, float* out, size_t ca
       info[7] = (int64_t)L.b_len;
       info[8] = L.CK;
       info[9] = L.kind == L_POST ? 0
+                : L.tile == hfg::kWsTile ? hfg::kWsMT
                 : L.prec == 1    ? hfg::kBf16x3Tiles[L.tile].MT()
                                  : kTiles[L.tile].MT();
     }
@@ -1089,9 +1155,9 @@ int hfg_debug_packed_resblock(hfg_handle* h, int stage, int j, float* out, size_
   if (stage < 0 || stage >= (int)h->stages.size()) return fail(HFG_EINVAL, "stage out of range");
   const Stage& st = h->stages[stage];
   for (int i = 0; i < 8; ++i) info[i] = 0;
-  if (!st.fused) return HFG_OK;
   if (j < 0 || j >= (int)st.rbs.size()) return fail(HFG_EINVAL, "resblock out of range");
   const RbFused& rb = st.rbs[j];
+  if (!rb.fused) return HFG_OK;
   info[0] = 1;
   info[1] = h->layers[rb.convs[0]].C_out;
   info[2] = rb.kt;

@@ -108,12 +108,27 @@ size_t bf16x3_lds_bytes(int tile, int kt, int dil);
 hipError_t launch_conv_bf16x3(int tile, int kt, bool ups, const ConvParams& p, int n_tiles,
                               int m_tiles, int batch, hipStream_t stream, const char** name);
 
+// ---- warp-specialized bf16x3 conv (conv_ws_bf16x3.hip) ----
+// 128 x 256 block tile, 4 consumer waves (64 x 128 each) + 4 producer waves; weights
+// streamed from global memory, packed [m_tile][wave_m][group][tap][wm][plane][lane][8].
+// Selected with tile id kWsTile in the host layer table.
+constexpr int kWsTile = 4;
+constexpr int kWsWaves = 8;
+constexpr int kWsMT = 128;
+constexpr int kWsNT = 256;
+bool ws_supported(int kt, bool ups, int M, int dil);
+size_t ws_lds_bytes(int kt, int dil);
+hipError_t launch_conv_ws_bf16x3(int kt, bool ups, const ConvParams& p, int n_tiles, int m_tiles,
+                                 int batch, hipStream_t stream, const char** name);
+
 // ---- whole ResBlock per launch (resblock_bf16x3.hip) ----
 // All 2*n_dil convs of one ResBlock of a C in {32, 64} stage on a window of
 // kRbColsPerWave * waves_n columns; x in registers, the conv operand in LDS.
 constexpr int kRbColsPerWave = 128;
 constexpr int kRbMaxConv = 16;
-constexpr int kRbMarg = 48;  // spare operand rows per side: every conv's (k-1)/2*dil <= this
+// spare operand rows per side (every conv's (k-1)/2*dil must fit): 48 for C <= 64, 28 for
+// C = 128 (its 256-column window then just fits the 160 KB LDS)
+constexpr int rb_marg(int C) { return C >= 128 ? 28 : 48; }
 struct RbParams {
   const float* x;        // stage input [B][C][L]
   int64_t bs;            // batch stride of x and mrf (C * L)

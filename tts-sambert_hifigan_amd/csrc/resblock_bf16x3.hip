@@ -53,9 +53,10 @@ resblock_bf16x3(const RbParams p) {
   constexpr int NWIN = 32 * WN * WAVES_N;  // window columns
   constexpr int STEPS = NG * KT;           // MFMA k-steps per conv
   static_assert(STEPS % 2 == 0, "two-deep A register ring needs an even step count");
-  // operand rows: the window plus kRbMarg spare rows on each side, read (never written)
+  // operand rows: the window plus MARG spare rows on each side, read (never written)
   // by the taps of edge columns; their contents only reach garbage columns
-  constexpr int ROWS = NWIN + 2 * kRbMarg;
+  constexpr int MARG = rb_marg(C);
+  constexpr int ROWS = NWIN + 2 * MARG;
   constexpr int PS = ROWS * 16;            // bytes per plane: [row][8 bf16]
   constexpr int HPS = 2 * PS;              // half-group (slots 0-7 | 8-15): hi, lo planes
   constexpr int GS = 2 * HPS;              // 16-channel group
@@ -129,7 +130,7 @@ resblock_bf16x3(const RbParams p) {
   }
 
   // lane's byte address of window column (cbase + col) in its half-group's hi plane
-  const int vb = half * HPS + (cbase + col + kRbMarg) * 16;
+  const int vb = half * HPS + (cbase + col + MARG) * 16;
 
   // B operand of the next conv: lrelu(v), zero outside [0, len), split hi/lo -> LDS.
   // The 8 accumulator rows a lane holds per 16-channel group are exactly the 8 slots
@@ -294,7 +295,8 @@ struct EntryRb {
   HFGRB_ENTRY(3, WMS, WNS), HFGRB_ENTRY(5, WMS, WNS), HFGRB_ENTRY(7, WMS, WNS), \
       HFGRB_ENTRY(11, WMS, WNS)
 
-EntryRb g_entriesRb[] = {HFGRB_KTS(2, 4), HFGRB_KTS(1, 8), HFGRB_KTS(1, 4)};
+EntryRb g_entriesRb[] = {HFGRB_KTS(2, 4), HFGRB_KTS(1, 8), HFGRB_KTS(1, 4),
+                         HFGRB_ENTRY(3, 4, 2)};
 
 }  // namespace
 
@@ -308,7 +310,7 @@ bool rb_supported(int C, int kt, int waves_n) {
 }
 
 size_t rb_lds_bytes(int C, int waves_n, int n_conv) {
-  const size_t rows = (size_t)kRbColsPerWave * waves_n + 2 * kRbMarg;
+  const size_t rows = (size_t)kRbColsPerWave * waves_n + 2 * rb_marg(C);
   return (size_t)C * rows * 4 + sizeof(float) * (size_t)n_conv * C;
 }
 
@@ -323,7 +325,7 @@ hipError_t launch_resblock_bf16x3(int C, int waves_n, int kt, const RbParams& p,
   if (p.n_conv < 2 || p.n_conv > kRbMaxConv || (p.n_conv & 1)) return hipErrorInvalidValue;
   if (p.W <= 0 || p.halo < 0 || p.W + 2 * p.halo > nwin) return hipErrorInvalidValue;
   for (int i = 0; i < p.n_conv; ++i)
-    if (p.dil[i] < 1 || (kt - 1) / 2 * p.dil[i] > kRbMarg) return hipErrorInvalidValue;
+    if (p.dil[i] < 1 || (kt - 1) / 2 * p.dil[i] > rb_marg(C)) return hipErrorInvalidValue;
   if (!e->name[0])
     snprintf(e->name, sizeof(e->name), "resblock_bf16x3<%d, %d, %d>", e->kt, e->waves_m,
              e->waves_n);
