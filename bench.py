@@ -42,7 +42,7 @@ PEAK_BF16_TFLOPS = 2500.0  # MI355X_MICROARCH.md: BF16 MFMA dense (no sparsity)
 
 def kernel_peak(name: str):
     """(peak in algorithmic fp32-conv TFLOP/s, description) for one kernel."""
-    if name.startswith("conv1d_bf16x3"):
+    if "bf16x3" in name:  # conv1d_bf16x3, resblock[16]_bf16x3, conv_ws_bf16x3
         # 3 bf16 MFMA products (hi*hi + hi*lo + lo*hi) per algorithmic multiply-add
         return PEAK_BF16_TFLOPS / 3.0, "bf16 dense MFMA 2.5 PFLOP/s / 3 split products"
     return PEAK_FP32_TFLOPS, "fp32 MFMA 157.3 TFLOP/s"

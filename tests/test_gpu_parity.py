@@ -95,10 +95,11 @@ def test_golden_fixture_bf16x3(pkg, golden_index, name):
     assert rel < 1e-3, rel
 
 
-@pytest.mark.parametrize("big_tile,fused,wn32",
-                         [("4", "1", "4"), ("4", "0", "8"), ("3", "1", "4"), ("0", "1", "8")])
+@pytest.mark.parametrize("big_tile,fused,wn32,m16",
+                         [("4", "1", "4", "1"), ("4", "0", "8", "0"), ("3", "1", "4", "1"),
+                          ("3", "1", "8", "0"), ("0", "1", "8", "1")])
 @pytest.mark.parametrize("preset,B,T", [("v1", 2, 300), ("v2star", 2, 200)])
-def test_bf16x3_vs_oracle_longer(pkg, preset, B, T, big_tile, fused, wn32, monkeypatch):
+def test_bf16x3_vs_oracle_longer(pkg, preset, B, T, big_tile, fused, wn32, m16, monkeypatch):
     """Random weights/mel vs the oracle, with each tile choice for the M >= 128 layers
     (HFG_BF16X3_BIGTILE: 0 = 128x256 8-wave, 3 = 128x256 4-wave, 4 = warp-specialized
     128x256, default) and with the
@@ -108,6 +109,7 @@ def test_bf16x3_vs_oracle_longer(pkg, preset, B, T, big_tile, fused, wn32, monke
     monkeypatch.setenv("HFG_BF16X3_BIGTILE", big_tile)
     monkeypatch.setenv("HFG_FUSED_RB", fused)
     monkeypatch.setenv("HFG_RB_WN32", wn32)
+    monkeypatch.setenv("HFG_MFMA16", m16)
     dev = _dev()
     cfg = C.PRESETS[preset]
     sd = C.make_state_dict(cfg, seed=7)
@@ -115,12 +117,13 @@ def test_bf16x3_vs_oracle_longer(pkg, preset, B, T, big_tile, fused, wn32, monke
     wav = _run(_gen(pkg, cfg, sd, dev, precision="bf16x3"), mel, dev)
     ref = _oracle(cfg, sd, mel)
     err = np.abs(wav - ref).max()
-    print(f"{preset} B={B} T={T} [bf16x3 fused={fused}]: max err {err:.3e}")
+    print(f"{preset} B={B} T={T} [bf16x3 tile={big_tile} fused={fused} m16={m16}]: "
+          f"max err {err:.3e}")
     assert err < ATOL
 
 
-@pytest.mark.parametrize("wn32", ["4", "8"])
-def test_fused_resblock_matches_layer_path(pkg, wn32, monkeypatch):
+@pytest.mark.parametrize("wn32,m16", [("4", "1"), ("8", "1"), ("4", "0")])
+def test_fused_resblock_matches_layer_path(pkg, wn32, m16, monkeypatch):
     """Whole-ResBlock kernel vs the layer-per-launch bf16x3 schedule on a ragged batch
     long enough for many windows per utterance (window seams, lengths that end inside
     a window, an utterance shorter than one window)."""
@@ -135,6 +138,7 @@ def test_fused_resblock_matches_layer_path(pkg, wn32, monkeypatch):
     for fused in ("0", "1"):
         monkeypatch.setenv("HFG_FUSED_RB", fused)
         monkeypatch.setenv("HFG_RB_WN32", wn32)
+        monkeypatch.setenv("HFG_MFMA16", m16)
         gen = _gen(pkg, cfg, sd, dev, precision="bf16x3")
         with torch.no_grad():
             outs.append(gen(mel, lengths=lens).cpu().numpy())

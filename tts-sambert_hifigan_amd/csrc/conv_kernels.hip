@@ -247,12 +247,28 @@ conv_post_tanh(const float* __restrict__ x, int64_t x_bs, int C, int L, const fl
     return;
   }
   for (int i = threadIdx.x; i < C * KP; i += TT) Ws[i] = w[i];
-  for (int c = 0; c < C; ++c) {
-    for (int t = threadIdx.x; t < XW; t += TT) {
-      const int gi = t0 - HALO + t;
-      float v = 0.f;
-      if (gi >= 0 && gi < Lb) v = lrelu(xb[(int64_t)c * L + gi]);
-      Xs[c * XW + t] = v;
+  // staging: each thread loads its column (and the first KP-1 threads one halo column)
+  // of CB channels at a time, all loads in flight before any use (one memory round trip
+  // per CB channels instead of one per channel)
+  constexpr int CB = 8;
+  const int tt = threadIdx.x;
+  const int gm = t0 - HALO + tt;       // main column
+  const int gh = t0 - HALO + TT + tt;  // halo column (tt < KP - 1), always >= 0
+  const bool okm = gm >= 0 && gm < Lb;
+  const bool okh = tt < KP - 1 && gh < Lb;
+  for (int c0 = 0; c0 < C; c0 += CB) {
+    float vm[CB], vh[CB];
+#pragma unroll
+    for (int e = 0; e < CB; ++e) {
+      const int64_t row = (int64_t)min(c0 + e, C - 1) * L;
+      vm[e] = xb[okm ? row + gm : 0];
+      vh[e] = xb[okh ? row + gh : 0];
+    }
+#pragma unroll
+    for (int e = 0; e < CB; ++e) {
+      if (c0 + e >= C) break;
+      Xs[(c0 + e) * XW + tt] = okm ? lrelu(vm[e]) : 0.f;
+      if (tt < KP - 1) Xs[(c0 + e) * XW + TT + tt] = okh ? lrelu(vh[e]) : 0.f;
     }
   }
   __syncthreads();

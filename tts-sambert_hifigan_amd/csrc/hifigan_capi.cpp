@@ -76,6 +76,7 @@ struct ProfRec {
 struct RbFused {
   std::vector<int> convs;     // layer indices in execution order conv1_0, conv2_0, conv1_1, ...
   bool fused = false;         // this ResBlock runs as one resblock_bf16x3 launch
+  bool m16 = false;           // ... on the 16x16x32 MFMA shape (resblock16_bf16x3)
   int kt = 0, halo = 0, W = 0, waves_n = 0;
   size_t w_off = 0, w_len = 0, b_off = 0, b_len = 0;  // in floats
 };
@@ -110,6 +111,7 @@ struct hfg_handle {
   bool use_fused_rb = true;  // whole-ResBlock kernel for C in {32, 64} (HFG_FUSED_RB=0 disables)
   int rb_waves_n32 = 4;      // window of the C = 32 ResBlock kernel: 128 * this columns
                              // (HFG_RB_WN32: 4 or 8)
+  bool mfma16 = true;        // 16x16x32-shape kernels where available (HFG_MFMA16=0: 32x32x16)
   int dbg_flags = 0;  // HFG_DEBUG_FLAGS env (kernel ablations; wrong results when set)
   std::vector<ProfRec> prof;
   std::vector<hipEvent_t> event_pool;
@@ -309,6 +311,8 @@ void build_layers(hfg_handle* h) {
       if (C == 128 && (double)nwin / rb.W > 1.15) ok = false;
       if (!ok) continue;
       rb.fused = true;
+      // 16x16x32 shape: measured 3-4% faster for C = 32, 2-10% slower for C >= 64 (r01)
+      rb.m16 = h->mfma16 && C == 32 && hfg::rb16_supported(C, rb.kt, waves_n);
       rb.w_off = off;
       rb.w_len = (size_t)rb.convs.size() * C * C * rb.kt;  // bf16 hi + lo = one float each
       off += (rb.w_len + 63) & ~(size_t)63;
@@ -417,6 +421,9 @@ void pack_bf16x3(const Layer& L, F wt, uint16_t* dst) {
 //   row = wave_m*32 + (lane & 31), ci = g*16 + 4*(lane >> 5) + (el & 3) + 8*(el >> 2)
 // (the permuted channel order of the kernel's operand planes); plane 0 = bf16(w),
 // plane 1 = bf16(w - hi).  Biases [conv][C].
+// A stream of resblock16_bf16x3 (16x16x32 shape):
+//   idx = ((((((wave_m*n_conv + e)*(C/32) + g)*KT + tap)*2 + i)*2 + plane)*64 + lane)*8 + el
+//   row = wave_m*32 + 16*i + (lane & 15), ci = g*32 + 16*(el >> 2) + 4*(lane >> 4) + (el & 3)
 void pack_resblock(hfg_handle* h, const RbFused& rb) {
   uint16_t* dst = reinterpret_cast<uint16_t*>(h->packed_host.data() + rb.w_off);
   float* bdst = h->packed_host.data() + rb.b_off;
@@ -424,7 +431,24 @@ void pack_resblock(hfg_handle* h, const RbFused& rb) {
   const int C = h->layers[rb.convs[0]].C_out;
   const int KT = rb.kt, n_g = C / 16;
   size_t idx = 0;
-  for (int wm = 0; wm < C / 32; ++wm)
+  for (int wm = 0; wm < C / 32 && rb.m16; ++wm)
+    for (int e = 0; e < n_conv; ++e) {
+      const Layer& L = h->layers[rb.convs[e]];
+      const float* w = h->params[L.mod + ".weight"].data.data();  // [C_out][C_in][k]
+      for (int g = 0; g < C / 32; ++g)
+        for (int tap = 0; tap < KT; ++tap)
+          for (int i = 0; i < 2; ++i)
+            for (int plane = 0; plane < 2; ++plane)
+              for (int lane = 0; lane < 64; ++lane)
+                for (int el = 0; el < 8; ++el) {
+                  const int row = wm * 32 + 16 * i + (lane & 15);
+                  const int ci = g * 32 + 16 * (el >> 2) + 4 * (lane >> 4) + (el & 3);
+                  const float v = w[((size_t)row * C + ci) * KT + tap];
+                  const uint16_t hi = f2bf(v);
+                  dst[idx++] = plane == 0 ? hi : f2bf(v - bf2f(hi));
+                }
+    }
+  for (int wm = 0; wm < C / 32 && !rb.m16; ++wm)
     for (int e = 0; e < n_conv; ++e) {
       const Layer& L = h->layers[rb.convs[e]];
       const float* w = h->params[L.mod + ".weight"].data.data();  // [C_out][C_in][k]
@@ -699,7 +723,9 @@ int run_resblock(hfg_handle* h, Launcher& ln, const RbFused& rb, const float* x,
   const double bytes = 4.0 * B * Lt * C * ((mrf_mode & 1) ? 3 : 2) + 4.0 * (double)rb.w_len;
   const char* name = nullptr;
   ln.begin(flop, bytes);
-  hipError_t e = hfg::launch_resblock_bf16x3(C, rb.waves_n, rb.kt, p, (int)B, ln.stream, &name);
+  hipError_t e =
+      rb.m16 ? hfg::launch_resblock16_bf16x3(C, rb.waves_n, rb.kt, p, (int)B, ln.stream, &name)
+             : hfg::launch_resblock_bf16x3(C, rb.waves_n, rb.kt, p, (int)B, ln.stream, &name);
   ln.end(name);
   if (e != hipSuccess)
     return fail(HFG_EIO, "launch resblock %s: %s", L0.mod.c_str(), hipGetErrorString(e));
@@ -888,6 +914,7 @@ int hfg_create(const hfg_config* cfg, int device, hfg_handle** out) {
     if (v == 0 || v == 3 || v == hfg::kWsTile) h->big_tile = v;
   }
   if (const char* fe = getenv("HFG_FUSED_RB")) h->use_fused_rb = atoi(fe) != 0;
+  if (const char* me = getenv("HFG_MFMA16")) h->mfma16 = atoi(me) != 0;
   if (const char* we = getenv("HFG_RB_WN32")) {
     const int v = atoi(we);
     if (v == 4 || v == 8) h->rb_waves_n32 = v;
@@ -1158,7 +1185,7 @@ int hfg_debug_packed_resblock(hfg_handle* h, int stage, int j, float* out, size_
   if (j < 0 || j >= (int)st.rbs.size()) return fail(HFG_EINVAL, "resblock out of range");
   const RbFused& rb = st.rbs[j];
   if (!rb.fused) return HFG_OK;
-  info[0] = 1;
+  info[0] = rb.m16 ? 2 : 1;  // 1: resblock_bf16x3 stream order, 2: resblock16_bf16x3
   info[1] = h->layers[rb.convs[0]].C_out;
   info[2] = rb.kt;
   info[3] = (int64_t)rb.convs.size();
