@@ -15,7 +15,9 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __attribute__((address_space(3))) void* lds_ptr_t3;
 typedef __attribute__((address_space(1))) void* gptr_t1;
 
-__device__ __forceinline__ float lrelu3(float v) { return v > 0.f ? v : v * kLReluSlope; }
+// leaky_relu(v, 0.1) as max(v, 0.1 v): bitwise the reference's select (slope < 1), two
+// VALU ops (v_mul + v_max) instead of compare + multiply + select
+__device__ __forceinline__ float lrelu3(float v) { return fmaxf(v, v * kLReluSlope); }
 
 // s_waitcnt vmcnt(N) with a compile-time N
 template <int N>

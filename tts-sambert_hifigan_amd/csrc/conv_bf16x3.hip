@@ -28,6 +28,11 @@
 
 namespace hfg {
 
+namespace {
+typedef float floatx2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+}  // namespace
+
 template <int KT_, int TPC, int WAVES_M, int WAVES_N, int WM, int WN, int WD, bool UPS>
 __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N, 2)
 conv1d_bf16x3(const ConvParams p) {
@@ -39,7 +44,8 @@ conv1d_bf16x3(const ConvParams p) {
   constexpr int TAP_ELEMS = 2 * WAVES_M * WM * 64 * 8;  // bf16 per tap of a slab (hi+lo)
   constexpr int SLAB = TPC * TAP_ELEMS;           // bf16 per chunk slab
   constexpr int KT_MAX = KT_ > 0 ? KT_ : 16;
-  constexpr int XW_MAX = NTILE + (KT_MAX - 1) * kMaxDil;
+  constexpr int XW_MAX = NTILE + ((KT_MAX - 1) * kMaxDil < kBf16x3MaxHalo
+                                       ? (KT_MAX - 1) * kMaxDil : kBf16x3MaxHalo);
   constexpr int XQ = (2 * XW_MAX + NT - 1) / NT;  // staging tasks per thread
   static_assert(XQ * 8 <= 32, "ok mask");
   constexpr int NX = XQ * 8;                      // input loads per thread per channel group
@@ -101,11 +107,14 @@ conv1d_bf16x3(const ConvParams p) {
   // time from a bit mask, so the loads' latency hides behind the chunk's MFMAs
   float xv[XQ][8];
   uint32_t xok = 0;
+  const int wave_u = __builtin_amdgcn_readfirstlane(wave);
   auto load_x = [&](int g) {
     const bool full = g * 16 + 16 <= p.C_in;  // block-uniform
     xok = 0;
 #pragma unroll
     for (int q = 0; q < XQ; ++q) {
+      // the last task row is mostly idle: a wave with no task in the window skips its loads
+      if (q == XQ - 1 && q > 0 && q * NT + wave_u * 64 >= 2 * XW) continue;
       const int i = tid + q * NT;
       const int t = i >> 1;
       const int cb = g * 16 + (i & 1) * 8;
@@ -133,12 +142,21 @@ conv1d_bf16x3(const ConvParams p) {
       if (i < 2 * XW) {
         bf16x8 h, l;
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          float v = (xok >> (q * 8 + e)) & 1u ? xv[q][e] : 0.f;
-          if (p.act_in) v = lrelu3(v);
-          const __bf16 hh = (__bf16)v;
-          h[e] = hh;
-          l[e] = (__bf16)(v - (float)hh);
+        for (int e = 0; e < 8; e += 2) {
+          floatx2 a;
+          a[0] = (xok >> (q * 8 + e)) & 1u ? xv[q][e] : 0.f;
+          a[1] = (xok >> (q * 8 + e + 1)) & 1u ? xv[q][e + 1] : 0.f;
+          if (p.act_in) {
+            a[0] = lrelu3(a[0]);
+            a[1] = lrelu3(a[1]);
+          }
+          const bf16x2 hh = __builtin_convertvector(a, bf16x2);
+          const floatx2 hf = __builtin_convertvector(hh, floatx2);
+          const bf16x2 ll = __builtin_convertvector(a - hf, bf16x2);
+          h[e] = hh[0];
+          h[e + 1] = hh[1];
+          l[e] = ll[0];
+          l[e + 1] = ll[1];
         }
         const int t = i >> 1;
         const int off = t * XROW + 8 * ((i & 1) ^ ((t >> 3) & 1));  // swizzled half
@@ -374,7 +392,8 @@ hipError_t launch_conv_bf16x3(int tile, int kt, bool ups, const ConvParams& p, i
   }
   if (!e) e = generic;
   if (!e) return hipErrorInvalidValue;
-  if (p.dil > kMaxDil || (e->kt == 0 && kt > 16)) return hipErrorInvalidValue;
+  if (p.dil > kMaxDil || (e->kt == 0 && kt > 16) || (kt - 1) * p.dil > kBf16x3MaxHalo)
+    return hipErrorInvalidValue;
   const Bf16x3Cfg& t = kBf16x3Tiles[tile];
   if (!e->name[0])
     snprintf(e->name, sizeof(e->name), "conv1d_bf16x3<%d, %d, %d, %d, %d, %d, %d, %s>", e->kt,

@@ -253,7 +253,7 @@ void build_layers(hfg_handle* h) {
       continue;
     }
     if (h->cfg.dtype == HFG_DTYPE_BF16X3 && (L.kind == L_CONV || L.kind == L_UPS) &&
-        hfg::bf16x3_tile_for_rows(L.M) >= 0) {
+        hfg::bf16x3_tile_for_rows(L.M) >= 0 && (L.KT - 1) * L.dil <= hfg::kBf16x3MaxHalo) {
       // split-precision path: chunk = 16 channels x TPC taps
       L.tile = hfg::bf16x3_tile_for_rows(L.M, h->big_tile == hfg::kWsTile ? 3 : h->big_tile);
       const hfg::Bf16x3Cfg& t3 = hfg::kBf16x3Tiles[L.tile];

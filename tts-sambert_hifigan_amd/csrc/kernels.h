@@ -101,6 +101,9 @@ constexpr int kBf16x3Tiles_n = 4;
 constexpr Bf16x3Cfg kBf16x3Tiles[kBf16x3Tiles_n] = {
     {2, 4, 2, 2, 4, 3}, {1, 4, 2, 2, 2, 2}, {1, 4, 1, 2, 4, 2}, {2, 2, 2, 4, 2, 2}};
 constexpr int kBf16x3Ck = 16;  // channels per chunk (one MFMA k-step per tap)
+// largest (KT-1)*dil window halo of the bf16x3 layer kernel (sizes its staging
+// registers: 3 tasks per thread for the 256-column tiles); wider layers run on the fp32 path
+constexpr int kBf16x3MaxHalo = 128;
 inline int bf16x3_tile_for_rows(int M, int big_tile = 0) {
   return M >= 128 ? big_tile : (M >= 64 ? 1 : (M >= 32 ? 2 : -1));
 }
