@@ -21,6 +21,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
+#include <type_traits>
 
 #include "bf16x3_common.h"
 #include "epilogue.h"
@@ -117,7 +118,8 @@ conv1d_bf16x3(const ConvParams p) {
       if (q == XQ - 1 && q > 0 && q * NT + wave_u * 64 >= 2 * XW) continue;
       const int i = tid + q * NT;
       const int t = i >> 1;
-      const int cb = g * 16 + (i & 1) * 8;
+      // (ablation bit7: always re-read channel group 0, i.e. L2-warm loads)
+      const int cb = ((p.dbg & 128) ? 0 : g) * 16 + (i & 1) * 8;
       const int gi = wbase + t;
       const bool tok = (i < 2 * XW) && ((unsigned)gi < (unsigned)L_in_b);
       // byte offsets from the block-uniform base: SGPR base + 32-bit VGPR offset loads
@@ -206,6 +208,55 @@ conv1d_bf16x3(const ConvParams p) {
       }
   };
 
+  // One tap of the 64x128-per-wave tile with the B fragments streamed per column tile
+  // (two in flight): only the A fragments stay live across the tap, which leaves room
+  // for the input staging interleaved into the same MFMA stream.
+  auto tap_stream = [&](const __bf16* Ws, const __bf16* Xh, int jj, int tap) {
+    const __bf16* Xl = Xh + xplane;
+    bf16x8 ah[WM], al[WM], bh[2], bl[2];
+#pragma unroll
+    for (int i = 0; i < WM; ++i) {
+      const __bf16* a = Ws + jj * TAP_ELEMS + (wave_m * WM + i) * 512 + lane * 8;
+      ah[i] = *reinterpret_cast<const bf16x8*>(a);
+      al[i] = *reinterpret_cast<const bf16x8*>(a + WAVES_M * WM * 512);
+    }
+    auto ldb = [&](int k) {
+      const int t = wave_n * 32 * WN + k * 32 + col + tap * p.dil;
+      const int off = t * XROW + 8 * (half ^ ((t >> 3) & 1));
+      bh[k & 1] = *reinterpret_cast<const bf16x8*>(Xh + off);
+      bl[k & 1] = *reinterpret_cast<const bf16x8*>(Xl + off);
+    };
+    ldb(0);
+#pragma unroll
+    for (int k = 0; k < WN; ++k) {
+      if (k + 1 < WN) ldb(k + 1);
+#pragma unroll
+      for (int i = 0; i < WM; ++i) {
+        acc[i][k] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[i], bh[k & 1], acc[i][k], 0, 0, 0);
+        acc[i][k] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bl[k & 1], acc[i][k], 0, 0, 0);
+        acc[i][k] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bh[k & 1], acc[i][k], 0, 0, 0);
+      }
+    }
+  };
+  // sched_group_barrier pattern for tap_stream + staging work in one basic block: the A
+  // reads and the first B pair, then per MFMA up to NV VALU (+ one VMEM load when LD),
+  // the next B pair after each column tile's first MFMA, a DS write every 4th MFMA (ST)
+  auto pin_stream = [&](auto nv_tag, auto ld_tag, auto st_tag) {
+    constexpr int NV = decltype(nv_tag)::value;
+    constexpr bool LD = decltype(ld_tag)::value, ST = decltype(st_tag)::value;
+    __builtin_amdgcn_sched_group_barrier(0x100, 2 * WM + 2, 0);
+#pragma unroll
+    for (int s = 0; s < 3 * WM * WN; ++s) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x002, NV, 0);
+      if (LD) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+      if (ST && s % 4 == 3) __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);
+      if (s % (3 * WM) == 0 && s / (3 * WM) + 1 < WN)
+        __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  };
+
   // ---- prologue: weight slabs of chunks 0..WD-2, input window of channel group 0 ----
   load_x(0);
 #pragma unroll
@@ -215,6 +266,68 @@ conv1d_bf16x3(const ConvParams p) {
   wait_vm<0>();
   lds_barrier();
 
+  if constexpr (KT_ > 0 && WM * WN >= 8) {
+    // ---- 64x128-per-wave tile, compile-time taps: the chunk loop unrolled over one
+    // channel group, so the chunks that stage the next input window are their own
+    // straight-line code.  That staging (the loads, or the conversion and LDS store)
+    // shares a basic block with the first tap's MFMAs and is interleaved into them: its
+    // VALU / memory issue hides under the matrix pipe instead of running as a serial
+    // phase in which both waves of a SIMD leave the pipe idle.  The last group re-stages
+    // itself into the idle buffer (no branch; one group of extra loads per block).
+    // Ablation bit0 (no restaging) is not available on this path.
+    static_assert(WD == 2, "fast path: two-slab weight ring");
+    constexpr int NTG = (KT_ + TPC - 1) / TPC;
+    constexpr int XG = NTG >= 2 ? NTG - 2 : 0;
+    using I6 = std::integral_constant<int, 6>;
+    using I3 = std::integral_constant<int, 3>;
+    using T_ = std::true_type;
+    using F_ = std::false_type;
+    const int NG = p.n_chunks / NTG;
+    int wslot = 0;
+    for (int g = 0; g < NG; ++g) {
+      const __bf16* Xh = Xbuf0 + (g & 1) * xbuf;
+      __bf16* const Xn = Xbuf0 + ((g + 1) & 1) * xbuf;
+      const int gn = min(g + 1, NG - 1);
+#pragma unroll
+      for (int tg = 0; tg < NTG; ++tg) {
+        const int c = g * NTG + tg;
+        const __bf16* Ws = Wbuf0 + wslot * SLAB;
+        const bool ISX = tg == XG, STX = tg == NTG - 1;
+        const int nt = KT_ - tg * TPC < TPC ? KT_ - tg * TPC : TPC;
+        const int tap0 = tg * TPC;
+        auto issue_next_w = [&]() {
+          issue_w(min(c + 1, p.n_chunks - 1), Wbuf0 + (wslot ^ 1) * SLAB);
+        };
+        if (STX && !ISX) {
+          // the slab DMA after the store: the input registers' vmcnt wait then does not
+          // also wait for the new slab
+          store_x(Xn);
+          tap_stream(Ws, Xh, 0, tap0);
+          pin_stream(I6{}, F_{}, T_{});
+          issue_next_w();
+        } else if (ISX && !STX) {
+          issue_next_w();
+          __builtin_amdgcn_sched_barrier(0);  // the slab DMA stays older than the input loads
+          load_x(gn);
+          tap_stream(Ws, Xh, 0, tap0);
+          pin_stream(I3{}, T_{}, F_{});
+        } else {
+          issue_next_w();
+          if (ISX) load_x(gn);
+          tap_stream(Ws, Xh, 0, tap0);
+          if (STX) store_x(Xn);
+        }
+#pragma unroll
+        for (int jj = 1; jj < TPC; ++jj)
+          if (jj < nt) tap_stream(Ws, Xh, jj, tap0 + jj);
+        // the slab of chunk c+1 must have landed; younger: this chunk's input loads
+        if (ISX && !STX) wait_vm<NX>();
+        else wait_vm<0>();
+        if (!(p.dbg & 4)) lds_barrier();
+        wslot ^= 1;
+      }
+    }
+  } else {
   // chunk c = (channel group g, tap group tg).  Weights: a ring of WD slabs, chunk c+WD-1
   // issued while chunk c is multiplied.  Input window: double-buffered per channel
   // group; group g+1's loads are issued at tap group xg = max(n_tg-2, 0) of group g
@@ -248,12 +361,8 @@ conv1d_bf16x3(const ConvParams p) {
     if constexpr (WM * WN >= 8) {
       // 64x128 per wave: one fragment set in flight (the accumulators hold 128 VGPRs)
 #pragma unroll
-      for (int jj = 0; jj < TPC; ++jj) {
-        if (jj < nt) {
-          load_frag(Ws, Xh, jj, tap0 + jj, f0);
-          mma(f0);
-        }
-      }
+      for (int jj = 0; jj < TPC; ++jj)
+        if (jj < nt) tap_stream(Ws, Xh, jj, tap0 + jj);
     } else {
       load_frag(Ws, Xh, 0, tap0, f0);
 #pragma unroll
@@ -275,6 +384,7 @@ conv1d_bf16x3(const ConvParams p) {
     else wait_vm<PW * (WD - 2)>();
     if (!(p.dbg & 4)) lds_barrier();
     if (++wslot == WD) wslot = 0;
+  }
   }
   if (p.dbg & 8) {  // ablation: no epilogue
     if (acc[0][0][0] == 1.2345e-30f) p.y[0] = acc[WM - 1][WN - 1][15];
