@@ -156,6 +156,16 @@ int hfg_forward_ex(hfg_handle* h, const float* mel, int64_t B, int64_t T,
  * (algorithmic FLOP and bytes) into buf. */
 int hfg_set_profiling(hfg_handle* h, int enable);
 int hfg_profile_reset(hfg_handle* h);
+
+/* Streams a forward spreads its batch over: 2 (default) runs a batch of B >= 2 as two
+ * halves, one on the caller's stream and one on an internal stream joined back by
+ * events (each utterance's wav is bitwise unchanged); 1 keeps every launch on the
+ * caller's stream.  Forwards under 4096 frames (B x T) stay on one stream.
+ * hfg_workspace_bytes depends on this setting.  With 2 streams the
+ * profile summary counts a layer's two half-batch dispatches as one launch whose time
+ * is the union of their intervals (the halves overlap other layers: per-kernel
+ * efficiency is measured with 1). */
+int hfg_set_streams(hfg_handle* h, int n);
 int hfg_profile_summary(hfg_handle* h, char* buf, size_t buflen);
 
 /* ---------------------------------------------------------------------------

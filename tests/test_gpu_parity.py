@@ -146,3 +146,31 @@ def test_fused_resblock_matches_layer_path(pkg, wn32, m16, monkeypatch):
     err = np.abs(outs[0] - outs[1]).max()
     print(f"fused vs layer path (wn32={wn32}): max diff {err:.3e}")
     assert err < 2e-5
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("precision", ["bf16x3", "fp32"])
+def test_two_stream_split_is_bitwise_equal(pkg, precision):
+    """hfg_set_streams(2) runs the batch halves on the caller's stream and an internal
+    one; every wav equals the 1-stream run bit for bit (odd batch, ragged lengths,
+    a batch large enough to be split: B x T >= 4096 frames)."""
+    from oracle import config as C, prng
+    dev = _dev()
+    cfg = C.V1
+    sd = C.make_state_dict(cfg, seed=17)
+    B, T = 5, 1000
+    mel = torch.as_tensor(prng.mel_input(23, (B, cfg.n_mels, T))).to(dev)
+    lens = torch.tensor([1000, 731, 1000, 2, 517], dtype=torch.int32, device=dev)
+    gen = _gen(pkg, cfg, sd, dev, precision=precision)
+    h = gen.hip_handle(dev)
+    outs = []
+    for n in (1, 2, 1):
+        h.set_streams(n)
+        with torch.no_grad():
+            outs.append((gen(mel).cpu().numpy(), gen(mel, lengths=lens).cpu().numpy()))
+        torch.cuda.synchronize()
+    h.set_streams(2)
+    for a, b in zip(outs[0], outs[1]):
+        assert np.array_equal(a, b)
+    for a, b in zip(outs[0], outs[2]):
+        assert np.array_equal(a, b)

@@ -122,6 +122,7 @@ SIGNATURES = {
     "hfg_forward_ex": (c_int, [c_void_p, c_void_p, c_int64, c_int64, POINTER(HfgForwardOpts),
                                c_void_p, c_int64, c_void_p, c_size_t, c_void_p]),
     "hfg_set_profiling": (c_int, [c_void_p, c_int]),
+    "hfg_set_streams": (c_int, [c_void_p, c_int]),
     "hfg_profile_reset": (c_int, [c_void_p]),
     "hfg_profile_summary": (c_int, [c_void_p, c_char_p, c_size_t]),
     "hfg_debug_packed_layer": (c_int, [c_void_p, c_char_p, POINTER(c_float), c_size_t,
@@ -211,6 +212,10 @@ class Handle:
         check(self.lib.hfg_forward_ex(self.ptr, c_void_p(mel_ptr), int(B), int(T), ctypes.byref(o),
                                       c_void_p(wav_ptr), int(out_len), c_void_p(ws_ptr),
                                       int(ws_bytes), c_void_p(stream)))
+
+    def set_streams(self, n: int):
+        """1: every launch on the caller's stream; 2: batch halves on two streams."""
+        check(self.lib.hfg_set_streams(self.ptr, int(n)))
 
     def set_profiling(self, on: bool):
         check(self.lib.hfg_set_profiling(self.ptr, 1 if on else 0))
