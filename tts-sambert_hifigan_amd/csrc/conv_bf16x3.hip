@@ -400,6 +400,11 @@ conv1d_bf16x3(const ConvParams p) {
     const int s_ = p.ups_s, p_ = p.ups_p;
     const bool vec4 = (s_ & 3) == 0 && (p_ & 3) == 0 && (p.L_out & 3) == 0;
     float* __restrict__ yb = p.y + (int64_t)b * p.y_bs;
+    // row -> (co, phase): a shift for the power-of-two rates (V1/V2: 8, 8, 2, 2) instead
+    // of an integer division per accumulator row
+    const bool pow2 = (s_ & (s_ - 1)) == 0;
+    const int sh = __builtin_ctz((unsigned)s_);
+    auto co_of = [&](int row) { return pow2 ? row >> sh : row / s_; };
 #pragma unroll
     for (int i = 0; i < WM; ++i) {
       const int rb = mt * MT + wave_m * 32 * WM + i * 32 + 4 * half;  // row of r = 0
@@ -415,7 +420,7 @@ conv1d_bf16x3(const ConvParams p) {
           for (int q = 0; q < 4; ++q) {
             const int row = rb + 8 * q;
             if (row >= p.M) continue;
-            const int co = row / s_;
+            const int co = co_of(row);
             const int t = n * s_ + (row - co * s_) - p_;
             float4 v;
             v.x = acc[i][k][4 * q + 0] + bv[4 * q + 0];
@@ -438,7 +443,7 @@ conv1d_bf16x3(const ConvParams p) {
         for (int r = 0; r < 16; ++r) {
           const int row = rb + (r & 3) + 8 * (r >> 2);
           if (row >= p.M) continue;
-          const int co = row / s_;
+          const int co = co_of(row);
           const int t = n * s_ + (row - co * s_) - p_;
           if (t >= 0 && t < L_out_b) yb[(int64_t)co * p.L_out + t] = acc[i][k][r] + bv[r];
         }
