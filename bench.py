@@ -10,9 +10,12 @@ mel and weights resident in HBM before the timed region.  Utterances are
 sharded over ranks (weak scaling); weights are generated on rank 0 and
 broadcast once with RCCL.  Rank 0 prints ONE JSON line.
 
-Roofline: every kernel launch in the timed region is bracketed by HIP events
-recorded on the launch stream (libhifigan_hip profiling mode); the dominant
-kernel's achieved TFLOP/s = its algorithmic FLOP ÷ its summed launch time.
+Timing: `value` is K uninstrumented steps of the production schedule (batch halves on
+two HIP streams).  Roofline: a second timed pass of the same K steps on one stream with
+every kernel launch bracketed by HIP events on that stream (libhifigan_hip profiling
+mode); the dominant kernel's achieved TFLOP/s = its algorithmic FLOP ÷ its summed
+launch time (with two streams the halves' intervals overlap, so they cannot be
+attributed to one kernel).
 cpu_baseline: the oracle's PyTorch-CPU restatement (same ATen ops as the
 reference) on this host's cores, rank 0 / N=1 only, on a bounded sample.
 """
@@ -234,7 +237,9 @@ def main():
             step()
         torch.cuda.synchronize(dev)
         profile = not args.no_profile
-        if profile:
+        # with 2 streams the timed loop runs uninstrumented (its per-launch intervals would
+        # overlap anyway); the per-kernel events come from the 1-stream pass below
+        if profile and args.streams == 1:
             h.profile_reset()
             h.set_profiling(True)
         if world > 1:
@@ -252,12 +257,13 @@ def main():
             elapsed = float(t.item())
         prof = {}
         if profile:
-            h.set_profiling(False)
-            prof = h.profile_summary()
-            if args.streams > 1:
+            if args.streams == 1:
+                h.set_profiling(False)
+                prof = h.profile_summary()
+            else:
                 # per-kernel times: with the batch halves overlapping, a dispatch's interval
-                # also covers the other half's kernels, so the roofline pass runs the same
-                # K steps on one stream (HIP events on that stream, as in the timed loop)
+                # also covers the other half's kernels, so the roofline pass times the same
+                # K steps again on one stream, every launch bracketed by HIP events on it
                 h.set_streams(1)
                 for _ in range(args.warmup):
                     step()
@@ -376,9 +382,10 @@ def main():
         }
         if args.precision in prof_ms:
             line["roofline"]["pass"] = (
-                "per-kernel HIP-event times from a 1-stream pass of the same K steps "
-                f"({prof_ms[args.precision]:.3f} ms/step; the timed value uses {args.streams} "
-                "streams, whose overlapping batch halves make per-kernel intervals overlap)")
+                "per-kernel HIP-event times from a second timed pass of the same K steps on "
+                f"1 stream ({prof_ms[args.precision]:.3f} ms/step); the value pass runs "
+                f"{args.streams} streams uninstrumented (overlapping batch halves make "
+                "per-kernel intervals overlap)")
         all_flop = sum(v["flop"] for v in prof.values()) / args.steps
         all_bytes = sum(v["bytes"] for v in prof.values()) / args.steps
         step_s = elapsed / args.steps
