@@ -113,7 +113,9 @@ struct hfg_handle {
   bool use_fused_rb = true;  // whole-ResBlock kernel for C in {32, 64} (HFG_FUSED_RB=0 disables)
   int rb_waves_n32 = 4;      // window of the C = 32 ResBlock kernel: 128 * this columns
                              // (HFG_RB_WN32: 4 or 8)
-  bool mfma16 = true;        // 16x16x32-shape kernels where available (HFG_MFMA16=0: 32x32x16)
+  bool mfma16 = true;        // 16x16x32-shape ResBlock kernel for C = 32 (HFG_MFMA16=0: off)
+  bool c16 = false;          // 16x16x32-shape wide layer kernel conv16_bf16x3 (HFG_C16=1;
+                             // parity-green, measured 26-45% slower than tile 3 on r01)
   int dbg_flags = 0;  // HFG_DEBUG_FLAGS env (kernel ablations; wrong results when set)
   // batch split over two HIP streams (HFG_SPLIT=1 disables): the two halves' launches
   // overlap, so one half's ramp-down / epilogue tail runs beside the other's main loops
@@ -261,6 +263,23 @@ void build_layers(hfg_handle* h) {
       continue;
     }
     if (h->cfg.dtype == HFG_DTYPE_BF16X3 && (L.kind == L_CONV || L.kind == L_UPS) &&
+        h->c16 && h->big_tile == 3 && L.M >= 128 &&
+        hfg::c16_supported(L.KT, L.kind == L_UPS, L.M, L.C_in, L.dil)) {
+      // 16x16x32-shape wide layer kernel: A per k-step of two (group, tap) entries
+      L.prec = 1;
+      L.tile = hfg::kC16Tile;
+      L.CK = hfg::kBf16x3Ck;
+      L.m_tiles = (L.M + hfg::kC16MT - 1) / hfg::kC16MT;
+      L.n_chunks = (L.C_in + 15) / 16 * L.KT / 2;  // k-steps (even group count)
+      L.w_off = off;
+      L.w_len = (size_t)L.m_tiles * L.n_chunks * 2 * hfg::kC16MT * 32 / 2;  // bf16 pairs
+      off += (L.w_len + 63) & ~(size_t)63;
+      L.b_off = off;
+      L.b_len = (size_t)L.m_tiles * hfg::kC16MT;
+      off += (L.b_len + 63) & ~(size_t)63;
+      continue;
+    }
+    if (h->cfg.dtype == HFG_DTYPE_BF16X3 && (L.kind == L_CONV || L.kind == L_UPS) &&
         hfg::bf16x3_tile_for_rows(L.M) >= 0 && (L.KT - 1) * L.dil <= hfg::kBf16x3MaxHalo) {
       // split-precision path: chunk = 16 channels x TPC taps
       L.tile = hfg::bf16x3_tile_for_rows(L.M, h->big_tile == hfg::kWsTile ? 3 : h->big_tile);
@@ -399,6 +418,32 @@ void pack_ws(const Layer& L, F wt, uint16_t* dst) {
               }
 }
 
+// A stream of conv16_bf16x3 (conv16_bf16x3.hip), in bf16 elements, per k-step s:
+//   idx = ((((((mt*P + s)*2 + plane)*2 + wave_m)*4 + i)*64 + lane)*8 + e
+//   row = mt*128 + wave_m*64 + i*16 + (lane & 15); entry f = 2s + (lane >> 5),
+//   g = f / KT, tap = f % KT, ci = g*16 + 8*((lane >> 4) & 1) + e.
+template <typename F>
+void pack_c16(const Layer& L, F wt, uint16_t* dst) {
+  const int P = L.n_chunks, KT = L.KT;
+  size_t idx = 0;
+  for (int mt = 0; mt < L.m_tiles; ++mt)
+    for (int s = 0; s < P; ++s)
+      for (int plane = 0; plane < 2; ++plane)
+        for (int wv = 0; wv < 2; ++wv)
+          for (int i = 0; i < 4; ++i)
+            for (int lane = 0; lane < 64; ++lane)
+              for (int e = 0; e < 8; ++e) {
+                const int row = mt * hfg::kC16MT + wv * 64 + i * 16 + (lane & 15);
+                const int f = 2 * s + (lane >> 5);
+                const int g = f / KT, tap = f % KT;
+                const int ci = g * 16 + 8 * ((lane >> 4) & 1) + e;
+                float v = 0.f;
+                if (row < L.M && ci < L.C_in) v = wt(row, ci, tap);
+                const uint16_t hi = f2bf(v);
+                dst[idx++] = plane == 0 ? hi : f2bf(v - bf2f(hi));
+              }
+}
+
 template <typename F>
 void pack_bf16x3(const Layer& L, F wt, uint16_t* dst) {
   const hfg::Bf16x3Cfg& t = hfg::kBf16x3Tiles[L.tile];
@@ -488,6 +533,23 @@ void pack_layer(hfg_handle* h, const Layer& L) {
   if (L.kind == L_POST) {
     std::memcpy(dst, w, sizeof(float) * L.C_in * 7);  // [1][C][7]
     bdst[0] = Bp.data[0];
+    return;
+  }
+  if (L.tile == hfg::kC16Tile) {
+    const int cin = L.C_in, k = L.k, s = L.s, Q = L.KT, cout = L.C_out;
+    if (L.kind == L_CONV)
+      pack_c16(L, [&](int row, int ci, int j) { return w[((size_t)row * cin + ci) * k + j]; },
+               reinterpret_cast<uint16_t*>(dst));
+    else
+      pack_c16(L,
+               [&](int row, int ci, int jj) {
+                 const int co = row / s, r = row % s;
+                 const int kidx = r + s * (Q - 1 - jj);
+                 return kidx < k ? w[((size_t)ci * cout + co) * k + kidx] : 0.f;
+               },
+               reinterpret_cast<uint16_t*>(dst));
+    for (size_t m = 0; m < L.b_len; ++m)
+      bdst[m] = m < (size_t)L.M ? Bp.data[L.kind == L_CONV ? m : m / s] : 0.f;
     return;
   }
   if (L.kind == L_CONV && L.tile == hfg::kWsTile) {
@@ -695,9 +757,10 @@ int run_conv(hfg_handle* h, Launcher& ln, const Layer& L, const float* x, int64_
   p.mrf_div = mrf_div;
   p.n_chunks = L.n_chunks;
   p.dbg = h->dbg_flags;
-  const int ntile = L.tile == hfg::kWsTile ? hfg::kWsNT
-                    : L.prec == 1          ? hfg::kBf16x3Tiles[L.tile].NTILE()
-                                           : kTiles[L.tile].NTILE();
+  const int ntile = L.tile == hfg::kWsTile    ? hfg::kWsNT
+                    : L.tile == hfg::kC16Tile ? hfg::kC16NT
+                    : L.prec == 1             ? hfg::kBf16x3Tiles[L.tile].NTILE()
+                                              : kTiles[L.tile].NTILE();
   const int n_tiles = (int)((Lt + ntile - 1) / ntile);
   const double flop = 2.0 * L.C_out * L.C_in * L.k * (double)Lt * B;
   double bytes = 4.0 * B * Lt * (L.C_in + L.C_out) + 4.0 * L.C_out * L.C_in * L.k;
@@ -708,6 +771,9 @@ int run_conv(hfg_handle* h, Launcher& ln, const Layer& L, const float* x, int64_
   hipError_t e = L.tile == hfg::kWsTile
                      ? hfg::launch_conv_ws_bf16x3(L.KT, false, p, n_tiles, L.m_tiles, (int)B,
                                                   ln.stream, &name)
+                 : L.tile == hfg::kC16Tile
+                     ? hfg::launch_conv16_bf16x3(L.KT, false, p, n_tiles, L.m_tiles, (int)B,
+                                                 ln.stream, &name)
                  : L.prec == 1
                      ? hfg::launch_conv_bf16x3(L.tile, L.KT, false, p, n_tiles, L.m_tiles, (int)B,
                                                ln.stream, &name)
@@ -784,9 +850,10 @@ int run_ups(hfg_handle* h, Launcher& ln, const Layer& L, const float* x, int64_t
   p.L_out = (int)Lout;
   p.n_chunks = L.n_chunks;
   p.dbg = h->dbg_flags;
-  const int ntile = L.tile == hfg::kWsTile ? hfg::kWsNT
-                    : L.prec == 1          ? hfg::kBf16x3Tiles[L.tile].NTILE()
-                                           : kTiles[L.tile].NTILE();
+  const int ntile = L.tile == hfg::kWsTile    ? hfg::kWsNT
+                    : L.tile == hfg::kC16Tile ? hfg::kC16NT
+                    : L.prec == 1             ? hfg::kBf16x3Tiles[L.tile].NTILE()
+                                              : kTiles[L.tile].NTILE();
   const int n_tiles = (p.N + ntile - 1) / ntile;
   const double flop = 2.0 * L.C_in * L.C_out * L.k * (double)Lin * B;
   const double bytes = 4.0 * B * (L.C_in * Lin + L.C_out * Lout) + 4.0 * L.C_in * L.C_out * L.k;
@@ -795,6 +862,9 @@ int run_ups(hfg_handle* h, Launcher& ln, const Layer& L, const float* x, int64_t
   hipError_t e = L.tile == hfg::kWsTile
                      ? hfg::launch_conv_ws_bf16x3(L.KT, true, p, n_tiles, L.m_tiles, (int)B,
                                                   ln.stream, &name)
+                 : L.tile == hfg::kC16Tile
+                     ? hfg::launch_conv16_bf16x3(L.KT, true, p, n_tiles, L.m_tiles, (int)B,
+                                                 ln.stream, &name)
                  : L.prec == 1
                      ? hfg::launch_conv_bf16x3(L.tile, L.KT, true, p, n_tiles, L.m_tiles, (int)B,
                                                ln.stream, &name)
@@ -978,6 +1048,7 @@ int hfg_create(const hfg_config* cfg, int device, hfg_handle** out) {
   }
   if (const char* fe = getenv("HFG_FUSED_RB")) h->use_fused_rb = atoi(fe) != 0;
   if (const char* me = getenv("HFG_MFMA16")) h->mfma16 = atoi(me) != 0;
+  if (const char* ce = getenv("HFG_C16")) h->c16 = atoi(ce) != 0;
   if (const char* se = getenv("HFG_SPLIT")) h->split = atoi(se);
   if (const char* we = getenv("HFG_RB_WN32")) {
     const int v = atoi(we);
@@ -1264,6 +1335,7 @@ int hfg_debug_packed_layer(hfg_handle* h, const char* mod, float* out, size_t ca
       info[8] = L.CK;
       info[9] = L.kind == L_POST ? 0
                 : L.tile == hfg::kWsTile ? hfg::kWsMT
+                : L.tile == hfg::kC16Tile ? hfg::kC16MT
                 : L.prec == 1    ? hfg::kBf16x3Tiles[L.tile].MT()
                                  : kTiles[L.tile].MT();
     }

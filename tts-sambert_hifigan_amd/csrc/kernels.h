@@ -124,6 +124,19 @@ size_t ws_lds_bytes(int kt, int dil);
 hipError_t launch_conv_ws_bf16x3(int kt, bool ups, const ConvParams& p, int n_tiles, int m_tiles,
                                  int batch, hipStream_t stream, const char** name);
 
+// ---- 16x16x32-shape wide layer kernel (conv16_bf16x3.hip) ----
+// 128 x 256 block tile, 4 waves of 64 x 128; K walked as (channel group, tap) entries two
+// per k-step; A packed per k-step [m_tile][step][plane][wave_m][row tile][lane][8].
+// Needs an even channel-group count and (KT-1)*dil <= kC16MaxHalo.
+constexpr int kC16Tile = 5;
+constexpr int kC16MT = 128;
+constexpr int kC16NT = 256;
+constexpr int kC16MaxHalo = 128;
+bool c16_supported(int kt, bool ups, int M, int C_in, int dil);
+size_t c16_lds_bytes(int kt, int dil);
+hipError_t launch_conv16_bf16x3(int kt, bool ups, const ConvParams& p, int n_tiles, int m_tiles,
+                                int batch, hipStream_t stream, const char** name);
+
 // ---- whole ResBlock per launch (resblock_bf16x3.hip) ----
 // All 2*n_dil convs of one ResBlock of a C in {32, 64} stage on a window of
 // kRbColsPerWave * waves_n columns; x in registers, the conv operand in LDS.
