@@ -176,3 +176,34 @@ def test_two_stream_split_is_bitwise_equal(pkg, precision):
         assert np.array_equal(a, b)
     for a, b in zip(outs[0], outs[2]):
         assert np.array_equal(a, b)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("big_tile,fused", [("3", "1"), ("3", "0"), ("0", "0")])
+def test_bf16x3_layer_kernels_run_to_run_bitwise(pkg, big_tile, fused, monkeypatch):
+    """Repeated forwards are bitwise identical on every bf16x3 layer-kernel tile (with the
+    whole-ResBlock kernel off the 64x256 / 32x256 tiles run every C <= 64 conv).  Guards
+    the per-wave vmcnt count of the staged input window: a wave that skips the idle last
+    staging row has 8 fewer loads in flight, and a wait that ignored that let a chunk read
+    a weight slab before its DMA landed (nondeterministic error up to ~6e-4)."""
+    from oracle import config as C, prng
+    monkeypatch.setenv("HFG_BF16X3_BIGTILE", big_tile)
+    monkeypatch.setenv("HFG_FUSED_RB", fused)
+    dev = _dev()
+    cfg = C.V1
+    sd = C.make_state_dict(cfg, seed=17)
+    B, T = 5, 1000
+    mel = torch.as_tensor(prng.mel_input(23, (B, cfg.n_mels, T))).to(dev)
+    lens = torch.tensor([1000, 731, 1000, 2, 517], dtype=torch.int32, device=dev)
+    gen = _gen(pkg, cfg, sd, dev, precision="bf16x3")
+    h = gen.hip_handle(dev)
+    outs = []
+    for n in (1, 2, 1, 2, 1, 2):
+        h.set_streams(n)
+        with torch.no_grad():
+            outs.append((gen(mel).cpu().numpy(), gen(mel, lengths=lens).cpu().numpy()))
+        torch.cuda.synchronize()
+    h.set_streams(2)
+    for o in outs[1:]:
+        for a, b in zip(outs[0], o):
+            assert np.array_equal(a, b), np.abs(a - b).max()

@@ -122,12 +122,15 @@ conv16_bf16x3(const ConvParams p) {
   // applied at the LDS store from a bit mask ----
   float xv[XQ][8];
   uint32_t xok = 0;
+  // a wave with no task in the last staging row skips its loads: 8 fewer in flight, which
+  // the vmcnt wait after the loading step must count (else it passes before the slab DMA)
+  const bool x_short = XQ > 1 && (XQ - 1) * NT + wave_u * 64 >= 2 * XW;
   auto load_x = [&](int g) {
     const bool full = g * 16 + 16 <= p.C_in;  // block-uniform
     xok = 0;
 #pragma unroll
     for (int q = 0; q < XQ; ++q) {
-      if (q == XQ - 1 && q > 0 && q * NT + wave_u * 64 >= 2 * XW) continue;
+      if (q == XQ - 1 && q > 0 && x_short) continue;
       const int i = tid + q * NT;
       const int t = i >> 1;
       const int cb = g * 16 + (i & 1) * 8;
@@ -286,7 +289,8 @@ conv16_bf16x3(const ConvParams p) {
       (void)I3{};
       // the slab of step s+1 must have landed; younger: input loads not yet stored
       const bool pending = (sp >= SCH.ld1 && sp < SCH.st1) || (sp >= SCH.ld2 && sp < SCH.st2);
-      if (pending) wait_vm<NX>();
+      if (pending && x_short) wait_vm<(NX >= 8 ? NX - 8 : 0)>();
+      else if (pending) wait_vm<NX>();
       else wait_vm<0>();
       lds_barrier();
     }

@@ -109,13 +109,24 @@ conv1d_bf16x3(const ConvParams p) {
   float xv[XQ][8];
   uint32_t xok = 0;
   const int wave_u = __builtin_amdgcn_readfirstlane(wave);
+  // a wave with no task in the (mostly idle) last staging row skips that row's loads, so
+  // it has 8 fewer input loads in flight than NX: every vmcnt wait that lets the input
+  // loads stay outstanding counts them per wave (wait_x), or it would pass before the
+  // older weight-slab DMA has landed
+  const bool x_short = XQ > 1 && (XQ - 1) * NT + wave_u * 64 >= 2 * XW;
+  auto wait_x = [&](auto n_tag) {
+    constexpr int N = decltype(n_tag)::value;
+    static_assert(XQ == 1 || N >= 8, "vmcnt");
+    if (x_short) wait_vm<(N >= 8 ? N - 8 : 0)>();
+    else wait_vm<N>();
+  };
   auto load_x = [&](int g) {
     const bool full = g * 16 + 16 <= p.C_in;  // block-uniform
     xok = 0;
 #pragma unroll
     for (int q = 0; q < XQ; ++q) {
       // the last task row is mostly idle: a wave with no task in the window skips its loads
-      if (q == XQ - 1 && q > 0 && q * NT + wave_u * 64 >= 2 * XW) continue;
+      if (q == XQ - 1 && q > 0 && x_short) continue;
       const int i = tid + q * NT;
       const int t = i >> 1;
       // (ablation bit7: always re-read channel group 0, i.e. L2-warm loads)
@@ -321,7 +332,7 @@ conv1d_bf16x3(const ConvParams p) {
         for (int jj = 1; jj < TPC; ++jj)
           if (jj < nt) tap_stream(Ws, Xh, jj, tap0 + jj);
         // the slab of chunk c+1 must have landed; younger: this chunk's input loads
-        if (ISX && !STX) wait_vm<NX>();
+        if (ISX && !STX) wait_x(std::integral_constant<int, NX>{});
         else wait_vm<0>();
         if (!(p.dbg & 4)) lds_barrier();
         wslot ^= 1;
@@ -353,7 +364,10 @@ conv1d_bf16x3(const ConvParams p) {
     // also wait for the new slab
     const bool w_late = WD > 2 && store_now;
     if (!w_late) issue_next_w();
-    if (issue_x) load_x(g + 1);  // after the slab DMA: a vmcnt can wait for it, not for these
+    // after the slab DMA (kept older by the sched barrier): a vmcnt can wait for it, not
+    // for these
+    __builtin_amdgcn_sched_barrier(0);
+    if (issue_x) load_x(g + 1);
     const int nt = taps_in(c);
     const int tap0 = tg * TPC;
     Frag f0, f1;
@@ -380,7 +394,7 @@ conv1d_bf16x3(const ConvParams p) {
     // the slab of chunk c+1 must have landed.  Younger than it: the slabs of chunks
     // c+2..c+WD-1 (PW pieces each) and this chunk's input loads when a later chunk
     // consumes them.
-    if (issue_x && !store_now) wait_vm<NX + PW * (WD - 2)>();
+    if (issue_x && !store_now) wait_x(std::integral_constant<int, NX + PW * (WD - 2)>{});
     else wait_vm<PW * (WD - 2)>();
     if (!(p.dbg & 4)) lds_barrier();
     if (++wslot == WD) wslot = 0;
