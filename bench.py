@@ -82,7 +82,8 @@ def parse():
 def cpu_baseline(cfg, sd, frames, budget_s):
     """Oracle (PyTorch-CPU restatement) on host cores: best of N runs of one
     [1, 80, frames] utterance after a warm-up, within ~budget_s seconds."""
-    from oracle import hifigan_torch, prng
+    from oracle import config as OC, hifigan_torch, prng  # the CPU baseline leg only
+    cfg = OC.GenConfig(**cfg.kwargs())
     threads = torch.get_num_threads()
     tsd = hifigan_torch.to_torch_state(sd)
     mel = torch.from_numpy(prng.mel_input(1234, (1, cfg.n_mels, frames)))
@@ -103,7 +104,7 @@ def cpu_baseline(cfg, sd, frames, budget_s):
             "rtf": best / (samples / SAMPLE_RATE)}
 
 
-def extra_configs(pkg, C, dev, precision, steps=5):
+def extra_configs(pkg, S, dev, precision, steps=5):
     """The other BASELINE.json configs, measured on this GPU (rank 0, N=1):
     C1 V1 [1,80,256] latency, eager vs a captured hipGraph replay (torch.cuda.graph
     around the same forward: 78 launches on the capture stream); C4 pinned V2*
@@ -123,12 +124,12 @@ def extra_configs(pkg, C, dev, precision, steps=5):
 
     def make(cfg):
         gen = pkg.HiFiGANGenerator(**cfg.kwargs(), precision=precision).eval()
-        gen.load_state_dict({k: torch.from_numpy(v) for k, v in C.make_state_dict(cfg, 0).items()})
+        gen.load_state_dict({k: torch.from_numpy(v) for k, v in S.random_state_dict(cfg).items()})
         return gen.to(dev)
 
     g = torch.Generator().manual_seed(1234)
     with torch.no_grad():
-        gen = make(C.V1)
+        gen = make(S.V1)
         mel = torch.randn(1, 80, 256, generator=g).to(dev)
         for _ in range(3):
             gen(mel)
@@ -150,7 +151,7 @@ def extra_configs(pkg, C, dev, precision, steps=5):
                                  "rtf_hipgraph": replay / (65536 / SAMPLE_RATE),
                                  "graph_equals_eager": ok}
         del gen
-        gen = make(C.V2STAR)
+        gen = make(S.V2STAR)
         mel = torch.randn(16, 80, 2048, generator=g).to(dev)
         for _ in range(2):
             gen(mel)
@@ -158,7 +159,7 @@ def extra_configs(pkg, C, dev, precision, steps=5):
         out["C4_v2star_16x80x2048"] = {"ms_per_step": t * 1e3, "samples_per_s": 16 * 2048 * 256 / t,
                                        "rtf": t / (16 * 2048 * 256 / SAMPLE_RATE)}
         del gen
-        gen = make(C.V1)
+        gen = make(S.V1)
         lens = [int(x) for x in torch.randint(60, 64, (32,), generator=g)]
         mel_pred = torch.randn(32, max(lens), 80, generator=g).to(dev)
         for _ in range(2):
@@ -194,11 +195,11 @@ def main():
     pkg.load_library()
     import importlib
     hdist = importlib.import_module(ge.PKG_NAME + ".dist")
-    from oracle import config as C, prng  # weight / input generators (test infrastructure)
+    S = importlib.import_module(ge.PKG_NAME + ".synth")  # random-init weights of the config
 
-    cfg = C.PRESETS[args.preset]
-    spec = [(k, s) for k, s, _ in C.param_specs(cfg)]
-    sd_np = C.make_state_dict(cfg, seed=0) if rank == 0 else None
+    cfg = S.PRESETS[args.preset]
+    spec = [(k, s) for k, s, _ in S.param_specs(cfg)]
+    sd_np = S.random_state_dict(cfg, seed=0) if rank == 0 else None
     coll_dev = dev if args.dist_backend == "nccl" else torch.device("cpu")
     if world > 1:
         sd = hdist.broadcast_state_dict({k: torch.from_numpy(v) for k, v in sd_np.items()}
@@ -314,8 +315,8 @@ def main():
                             "hi + lo, products hi*hi + hi*lo + lo*hi on the bf16 MFMA (the "
                             "upsamplers too); wav within 1e-4 of the reference on every golden "
                             "fixture (max 9e-6), tests/test_gpu_parity.py"),
-        "data": "synthetic: mel ~ N(0,1) (torch seed 1234), PRNG default-init V1 weights "
-                "(no checkpoint)",
+        "data": "synthetic: mel ~ N(0,1) (torch seed 1234), random default-init weights "
+                "U(+-1/sqrt(fan_in)) of the preset (synth.py; no checkpoint ships)",
         "config": {
             "workload": f"HiFi-GAN {args.preset.upper()} Generator forward, mel [{args.batch},"
                         f"{cfg.n_mels},{T}] per GPU -> wav [{args.batch},1,{out_len}]",
@@ -395,16 +396,30 @@ def main():
             "hbm_model_GBs": all_bytes / step_s / 1e9,
             "hbm_model_frac": all_bytes / step_s / 1e9 / PEAK_HBM_GBS,
             "kernel_time_ms": tot_ms,
-            "note": "algorithmic FLOP / layer-streaming bytes (SURVEY.md §8(d)) per step / step time",
+            "note": "algorithmic FLOP and the per-launch algorithmic bytes of the kernels as "
+                    "launched (a whole-ResBlock launch counts only its own input, output and "
+                    "weights) per step / step time",
+        }
+        # SURVEY.md §8(d) canonical layer-streaming byte model (fp32, every conv streams
+        # its input and output, weights once per forward): the north-star HBM-roofline figure
+        bpf = S.layer_streaming_bytes_per_frame(cfg)
+        gpu_bytes = B * T * bpf + S.param_bytes(cfg)  # per GPU per step
+        line["roofline_step"]["hbm_canonical"] = {
+            "bytes_per_frame": bpf,
+            "bytes_per_sample": gpu_bytes / (B * out_len),
+            "GBs_per_gpu": gpu_bytes / step_s / 1e9,
+            "frac": gpu_bytes / step_s / 1e9 / PEAK_HBM_GBS,
+            "note": "equivalent bandwidth of the layer-streaming model at the measured step "
+                    "time; the fused kernels move fewer bytes (PMC traffic in roofline)",
         }
         line["kernels"] = {k: {"launches": v["launches"] // args.steps,
                                "ms_per_step": v["ms"] / args.steps,
                                "TFLOPs": v["flop"] / (v["ms"] * 1e-3) / 1e12 if v["ms"] else None}
                            for k, v in sorted(prof.items(), key=lambda kv: -kv[1]["ms"])}
     if world == 1 and not args.no_extra:
-        line["extra_configs"] = extra_configs(pkg, C, dev, args.precision)
+        line["extra_configs"] = extra_configs(pkg, S, dev, args.precision)
     if world == 1 and not args.no_cpu_baseline:
-        cfg_np = C.make_state_dict(cfg, seed=0) if sd_np is None else sd_np
+        cfg_np = S.random_state_dict(cfg, seed=0) if sd_np is None else sd_np
         line["cpu_baseline"] = cpu_baseline(cfg, cfg_np, T, args.cpu_budget_s)
         line["cpu_baseline"]["gpu_over_cpu"] = value / line["cpu_baseline"]["value"]
     print(json.dumps(line), flush=True)
