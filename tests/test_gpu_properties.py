@@ -249,3 +249,48 @@ def test_full_size_bf16x3_batch_split_invariance(full_bf16x3, dev):
     assert torch.equal(one[0], wav[3])
     five = run(gen, mel[1:6].to(dev))
     assert torch.equal(five, wav[1:6])
+
+
+# ---- maximum size ------------------------------------------------------------------
+T_MAX = 131072  # V1: 8192 * T fp32 per item = 2^30 elements, the kernels' 32-bit byte offsets
+
+
+@pytest.mark.parametrize("precision", ["bf16x3", "fp32"])
+def test_max_length_utterance_windowed_oracle(pkg, dev, precision):
+    """One utterance at the longest T the C ABI accepts (2^30 activation elements per
+    item, ~25 min of audio): the output at the head, the middle and the very end matches
+    the oracle on a receptive-field window, so no byte offset wraps."""
+    from oracle import config as C, hifigan_torch as H
+    sd = C.make_state_dict(C.V1, seed=0)
+    gen = pkg.HiFiGANGenerator(**C.V1.kwargs(), precision=precision).eval()
+    gen.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
+    gen = gen.to(dev)
+    g = torch.Generator().manual_seed(77)
+    mel = torch.randn(1, 80, T_MAX, generator=g)
+    wav = run(gen, mel.to(dev))
+    assert wav.shape == (1, 1, T_MAX * 256)
+    W, M = 32, 16
+    tsd = H.to_torch_state(sd)
+    for start in (0, T_MAX // 2 + 5, T_MAX - W):
+        a, b = max(0, start - M), min(T_MAX, start + W + M)
+        ref = H.generator_forward(tsd, C.V1, mel[:, :, a:b])
+        ref = ref[0, 0, (start - a) * 256:(start - a + W) * 256].numpy()
+        got = wav[0, 0, start * 256:(start + W) * 256].cpu().numpy()
+        assert np.abs(got - ref).max() < ATOL, (precision, start)
+    del wav
+    torch.cuda.empty_cache()
+
+
+def test_over_max_length_rejected(pkg, v1, dev):
+    """One frame past the limit is refused with EINVAL before any launch."""
+    gen, _ = v1
+    h = gen.hip_handle(dev)
+    lib = pkg.load_library()
+    T = T_MAX + 1
+    L = lib.hfg_out_len(h.ptr, T)
+    dummy = torch.empty(64, device=dev)
+    rc = lib.hfg_forward_ws(h.ptr, ctypes.c_void_p(dummy.data_ptr()), 1, T,
+                            ctypes.c_void_p(dummy.data_ptr()), L, ctypes.c_void_p(dummy.data_ptr()),
+                            256, None)
+    assert rc == -22
+    assert b"exceeds 2^30" in lib.hfg_last_error()

@@ -647,6 +647,7 @@ int do_commit(hfg_handle* h) {
 struct Shapes {
   std::vector<int64_t> L;  // L[0] = T, L[i+1] = length after stage i
   int64_t buf_elems;       // per-buffer elements (all B items)
+  int64_t item_elems;      // largest per-item activation (max over stages of C * L)
 };
 
 Shapes shapes_for(const hfg_handle* h, int64_t B, int64_t T) {
@@ -661,6 +662,7 @@ Shapes shapes_for(const hfg_handle* h, int64_t B, int64_t T) {
     s.L.push_back(lo);
     mx = std::max(mx, (int64_t)(h->cfg.c0 >> (i + 1)) * std::max<int64_t>(lo, 0));
   }
+  s.item_elems = mx;
   s.buf_elems = ((mx * B + 63) / 64) * 64;
   return s;
 }
@@ -891,8 +893,11 @@ int forward_impl(hfg_handle* h, const float* mel, int64_t B, int64_t T, const hf
   if (sh.L.back() != out_len)
     return fail(HFG_EINVAL, "out_len %lld != expected %lld", (long long)out_len,
                 (long long)sh.L.back());
-  if ((double)sh.buf_elems / (double)B * 1.0 > 2147483647.0)
-    return fail(HFG_EINVAL, "per-item activation exceeds 2^31 elements");
+  // the kernels address one utterance's activations with 32-bit byte offsets from a
+  // per-item base: at most 2^30 fp32 elements per item (V1: T <= 131072 frames)
+  if (sh.item_elems > ((int64_t)1 << 30))
+    return fail(HFG_EINVAL, "per-item activation of %lld elements exceeds 2^30 (T too long)",
+                (long long)sh.item_elems);
   if (ws_len < ws_part_bytes(h, B, T)) return fail(HFG_EINVAL, "workspace too small");
   float* buf[4];
   for (int i = 0; i < 4; ++i) buf[i] = reinterpret_cast<float*>(ws) + (size_t)i * sh.buf_elems;
