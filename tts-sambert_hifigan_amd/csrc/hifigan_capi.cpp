@@ -110,7 +110,8 @@ struct hfg_handle {
   bool profiling = false;
   int big_tile = 3;  // bf16x3 tile for M >= 128 (HFG_BF16X3_BIGTILE env: 0, 3 or 4 =
                      // warp-specialized conv_ws_bf16x3, measured ~3-15% slower than 3 on r01)
-  bool use_fused_rb = true;  // whole-ResBlock kernel for C in {32, 64} (HFG_FUSED_RB=0 disables)
+  bool use_fused_rb = true;
+  bool rb64_narrow = true;   // 256-column whole-ResBlock window for C = 64, k = 3 (HFG_RB64_NARROW=0 disables)  // whole-ResBlock kernel for C in {32, 64} (HFG_FUSED_RB=0 disables)
   int rb_waves_n32 = 4;      // window of the C = 32 ResBlock kernel: 128 * this columns
                              // (HFG_RB_WN32: 4 or 8)
   bool mfma16 = true;        // 16x16x32-shape ResBlock kernel for C = 32 (HFG_MFMA16=0: off)
@@ -318,12 +319,16 @@ void build_layers(hfg_handle* h) {
     st.rbs.assign(c.n_res, RbFused{});
     if (h->cfg.dtype != HFG_DTYPE_BF16X3 || !h->use_fused_rb || (C != 32 && C != 64 && C != 128))
       continue;
-    const int waves_n = C == 128 ? 2 : C == 64 ? 4 : h->rb_waves_n32;
-    const int nwin = hfg::kRbColsPerWave * waves_n;
     int idx = 0;
     for (int j = 0; j < c.n_res; ++j) {
       RbFused rb;
       rb.kt = c.res_kernels[j];
+      // C = 64, k = 3: a 256-column window (5 % more halo recompute than 512) whose small
+      // LDS footprint lets two blocks share a CU and overlap their operand rewrites
+      const int waves_n = C == 128 ? 2
+                          : C == 64  ? (rb.kt == 3 && h->rb64_narrow ? 2 : 4)
+                                     : h->rb_waves_n32;
+      const int nwin = hfg::kRbColsPerWave * waves_n;
       rb.waves_n = waves_n;
       bool ok = rb.kt % 2 == 1 && hfg::rb_supported(C, rb.kt, waves_n) &&
                 2 * c.n_dil[j] <= hfg::kRbMaxConv;
@@ -331,7 +336,7 @@ void build_layers(hfg_handle* h) {
         rb.convs.push_back(st.conv1[idx]);
         rb.convs.push_back(st.conv2[idx]);
         rb.halo += (rb.kt - 1) / 2 * c.dil[j][m] + (rb.kt - 1) / 2;
-        if ((rb.kt - 1) / 2 * c.dil[j][m] > hfg::rb_marg(C)) ok = false;
+        if ((rb.kt - 1) / 2 * c.dil[j][m] > hfg::rb_marg(C, waves_n)) ok = false;
       }
       rb.W = nwin - 2 * rb.halo;
       if (rb.W < nwin / 4) ok = false;
@@ -1055,6 +1060,7 @@ int hfg_create(const hfg_config* cfg, int device, hfg_handle** out) {
   if (const char* me = getenv("HFG_MFMA16")) h->mfma16 = atoi(me) != 0;
   if (const char* ce = getenv("HFG_C16")) h->c16 = atoi(ce) != 0;
   if (const char* se = getenv("HFG_SPLIT")) h->split = atoi(se);
+  if (const char* rn = getenv("HFG_RB64_NARROW")) h->rb64_narrow = atoi(rn) != 0;
   if (const char* we = getenv("HFG_RB_WN32")) {
     const int v = atoi(we);
     if (v == 4 || v == 8) h->rb_waves_n32 = v;

@@ -143,8 +143,11 @@ hipError_t launch_conv16_bf16x3(int kt, bool ups, const ConvParams& p, int n_til
 constexpr int kRbColsPerWave = 128;
 constexpr int kRbMaxConv = 16;
 // spare operand rows per side (every conv's (k-1)/2*dil must fit): 48 for C <= 64, 28 for
-// C = 128 (its 256-column window then just fits the 160 KB LDS)
-constexpr int rb_marg(int C) { return C >= 128 ? 28 : 48; }
+// C = 128 (its 256-column window then just fits the 160 KB LDS), 16 for the narrow C = 64
+// window (256 columns: 74 KB, two blocks per CU, used for k = 3)
+constexpr int rb_marg(int C, int waves_n) {
+  return C >= 128 ? 28 : (C == 64 && waves_n == 2) ? 16 : 48;
+}
 struct RbParams {
   const float* x;        // stage input [B][C][L]
   int64_t bs;            // batch stride of x and mrf (C * L)

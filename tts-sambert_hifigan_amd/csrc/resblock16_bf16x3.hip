@@ -54,7 +54,7 @@ resblock16_bf16x3(const RbParams p) {
   constexpr int PF = 3;                    // B fragments prefetched this many units ahead
   constexpr int NB = 4;                    // B ring (WN % NB == 0: slot = column tile % NB)
   static_assert(WN % NB == 0 && PF < NB, "B ring");
-  constexpr int MARG = rb_marg(C);
+  constexpr int MARG = rb_marg(C, WAVES_N);
   constexpr int ROWS = NWIN + 2 * MARG;
   constexpr int PS = ROWS * 16;            // bytes per plane: [row][8 bf16]
   constexpr int QS = 2 * PS;               // per quarter: hi, lo planes
@@ -374,7 +374,7 @@ hipError_t launch_resblock16_bf16x3(int C, int waves_n, int kt, const RbParams& 
   if (p.n_conv < 2 || p.n_conv > kRbMaxConv || (p.n_conv & 1)) return hipErrorInvalidValue;
   if (p.W <= 0 || p.halo < 0 || p.W + 2 * p.halo > nwin) return hipErrorInvalidValue;
   for (int i = 0; i < p.n_conv; ++i)
-    if (p.dil[i] < 1 || (kt - 1) / 2 * p.dil[i] > rb_marg(C)) return hipErrorInvalidValue;
+    if (p.dil[i] < 1 || (kt - 1) / 2 * p.dil[i] > rb_marg(C, waves_n)) return hipErrorInvalidValue;
   if (!e->name[0])
     snprintf(e->name, sizeof(e->name), "resblock16_bf16x3<%d, %d, %d>", e->kt, e->waves_m,
              e->waves_n);

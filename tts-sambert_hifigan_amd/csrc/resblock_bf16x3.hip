@@ -55,7 +55,7 @@ resblock_bf16x3(const RbParams p) {
   static_assert(STEPS % 2 == 0, "two-deep A register ring needs an even step count");
   // operand rows: the window plus MARG spare rows on each side, read (never written)
   // by the taps of edge columns; their contents only reach garbage columns
-  constexpr int MARG = rb_marg(C);
+  constexpr int MARG = rb_marg(C, WAVES_N);
   constexpr int ROWS = NWIN + 2 * MARG;
   constexpr int PS = ROWS * 16;            // bytes per plane: [row][8 bf16]
   constexpr int HPS = 2 * PS;              // half-group (slots 0-7 | 8-15): hi, lo planes
@@ -296,7 +296,7 @@ struct EntryRb {
       HFGRB_ENTRY(11, WMS, WNS)
 
 EntryRb g_entriesRb[] = {HFGRB_KTS(2, 4), HFGRB_KTS(1, 8), HFGRB_KTS(1, 4),
-                         HFGRB_ENTRY(3, 4, 2)};
+                         HFGRB_ENTRY(3, 4, 2), HFGRB_ENTRY(3, 2, 2)};
 
 }  // namespace
 
@@ -310,7 +310,7 @@ bool rb_supported(int C, int kt, int waves_n) {
 }
 
 size_t rb_lds_bytes(int C, int waves_n, int n_conv) {
-  const size_t rows = (size_t)kRbColsPerWave * waves_n + 2 * rb_marg(C);
+  const size_t rows = (size_t)kRbColsPerWave * waves_n + 2 * rb_marg(C, waves_n);
   return (size_t)C * rows * 4 + sizeof(float) * (size_t)n_conv * C;
 }
 
@@ -325,7 +325,7 @@ hipError_t launch_resblock_bf16x3(int C, int waves_n, int kt, const RbParams& p,
   if (p.n_conv < 2 || p.n_conv > kRbMaxConv || (p.n_conv & 1)) return hipErrorInvalidValue;
   if (p.W <= 0 || p.halo < 0 || p.W + 2 * p.halo > nwin) return hipErrorInvalidValue;
   for (int i = 0; i < p.n_conv; ++i)
-    if (p.dil[i] < 1 || (kt - 1) / 2 * p.dil[i] > rb_marg(C)) return hipErrorInvalidValue;
+    if (p.dil[i] < 1 || (kt - 1) / 2 * p.dil[i] > rb_marg(C, waves_n)) return hipErrorInvalidValue;
   if (!e->name[0])
     snprintf(e->name, sizeof(e->name), "resblock_bf16x3<%d, %d, %d>", e->kt, e->waves_m,
              e->waves_n);
