@@ -1,10 +1,10 @@
 """Diagnostic (GPU): 1-stream vs 2-stream and run-to-run bitwise equality of the
 Generator, per precision, with and without ragged lengths.
-usage: python profiles/diag_split.py"""
+usage: python tests/tools/diag_split.py"""
 import os, sys
 import numpy as np
 import torch
-ROOT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..")
+ROOT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "..")
 sys.path.insert(0, ROOT)
 import __graft_entry__ as ge
 from oracle import config as C, prng

@@ -9,7 +9,7 @@ cheaper scheme before building it.  Research script (not product, not a test).
   fp8x_lo  : bf16 hi*hi + hi*lo in bf16 + lo(x)*hi(w) in fp8 (cross term of the
              activations only in fp8)
 
-usage: python profiles/research/emulate_fp8_cross.py
+usage: python tests/tools/emulate_fp8_cross.py
 """
 import os
 import sys

@@ -2,7 +2,7 @@
 (each with its own workspace), to see whether overlapping the halves' launch tails
 pays.  Prints one JSON line.  Not part of the product path.
 
-    python profiles/exp_two_streams.py
+    python tests/tools/exp_two_streams.py
 """
 import json
 import os
@@ -11,7 +11,7 @@ import time
 
 import torch
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, ROOT)
 import __graft_entry__ as ge  # noqa: E402
 from oracle import config as C  # noqa: E402
