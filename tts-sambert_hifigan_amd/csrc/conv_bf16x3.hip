@@ -428,6 +428,27 @@ conv1d_bf16x3(const ConvParams p) {
 #pragma unroll
       for (int k = 0; k < WN; ++k) {
         const int n = n0 + wave_n * 32 * WN + k * 32 + col;
+        // wave-uniform interior test (the whole 32-column x 32-row tile lands inside
+        // [0, L_out)): unmasked float4 stores, one instruction each (the masked path
+        // below compiles to a tail-merged dwordx3 + dword pair)
+        const int nt_u = n0 + (wave_u / WAVES_M) * 32 * WN + k * 32;
+        const int rt_u = mt * MT + (wave_u % WAVES_M) * 32 * WM + i * 32;
+        if (vec4 && rt_u + 31 < p.M && nt_u + 31 < N_b && nt_u * s_ - p_ >= 0 &&
+            (nt_u + 32) * s_ - 1 - p_ < L_out_b) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int row = rb + 8 * q;
+            const int co = co_of(row);
+            const int t = n * s_ + (row - co * s_) - p_;
+            float4 v;
+            v.x = acc[i][k][4 * q + 0] + bv[4 * q + 0];
+            v.y = acc[i][k][4 * q + 1] + bv[4 * q + 1];
+            v.z = acc[i][k][4 * q + 2] + bv[4 * q + 2];
+            v.w = acc[i][k][4 * q + 3] + bv[4 * q + 3];
+            *reinterpret_cast<float4*>(yb + (int64_t)co * p.L_out + t) = v;
+          }
+          continue;
+        }
         if (n >= N_b) continue;
         if (vec4) {
 #pragma unroll
