@@ -27,6 +27,10 @@ __device__ __forceinline__ void conv_epilogue(const ConvParams& p, const float* 
   const bool add_mrf = p.mrf && (p.mrf_mode & 1);
   const bool div_mrf = p.mrf && (p.mrf_mode & 2);
   const bool act = p.act_out != 0;
+  // the tile origin is wave-uniform: a tile wholly inside [0, M) x [0, N_b) stores
+  // without per-element exec-mask branches
+  const int row_u = __builtin_amdgcn_readfirstlane(row_base);
+  const int n_u = __builtin_amdgcn_readfirstlane(n_base);
   // bias: padded to the m-tile, every row index is readable
 #pragma unroll
   for (int i = 0; i < WM; ++i) {
@@ -70,9 +74,14 @@ __device__ __forceinline__ void conv_epilogue(const ConvParams& p, const float* 
 #pragma unroll
         for (int r = 0; r < 16; ++r) v[r] = v[r] / p.mrf_div;
       }
+      if (n_u + k * 32 + 31 < N_b && row_u + i * 32 + 31 < p.M) {
 #pragma unroll
-      for (int r = 0; r < 16; ++r)
-        if (ok[r]) *reinterpret_cast<float*>(outb + off[r]) = v[r];
+        for (int r = 0; r < 16; ++r) *reinterpret_cast<float*>(outb + off[r]) = v[r];
+      } else {
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          if (ok[r]) *reinterpret_cast<float*>(outb + off[r]) = v[r];
+      }
     }
   }
 }
