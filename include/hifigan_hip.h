@@ -18,6 +18,11 @@
  *   hfg_forward_ex      ← acoustic→vocoder glue (spec-only in the reference,
  *                         .kiro/specs/.../design.md:905-906): [B,T,80] input
  *                         and per-utterance lengths of a padded batch
+ *   hfg_mrf_create      ← MRF.__init__ / ResBlock.__init__  models/hifigan.py:96-114, 34-70
+ *   hfg_mrf_forward     ← MRF.forward                       models/hifigan.py:116-131
+ *   hfg_resblock_forward← ResBlock.forward                  models/hifigan.py:72-86
+ *   hfg_checksum32      ← (no reference counterpart) content hash the Python
+ *                         module uses to notice in-place parameter edits
  *
  * Conventions
  *   - Every int-returning call returns 0 on success or a negative errno-style
@@ -30,9 +35,10 @@
  *     passed as void*; NULL = default stream): no host synchronisation and no
  *     allocation when weights are committed and the workspace is large enough,
  *     so it may be captured into a hipGraph.
- *   - One handle per device.  A handle is not thread-safe; hfg_forward with
- *     the internal workspace must not run concurrently on two streams —
- *     use hfg_forward_ws with a per-stream workspace for that.
+ *   - One handle per device.  Calls on one handle are serialised by a
+ *     per-handle lock (a forward enqueues its launches, then releases it);
+ *     hfg_forward with the internal workspace must not be used from two
+ *     streams at once — use hfg_forward_ws with a per-stream workspace.
  */
 #ifndef HIFIGAN_HIP_H
 #define HIFIGAN_HIP_H
@@ -55,14 +61,17 @@ extern "C" {
 #define HFG_EAGAIN (-11)   /* weights incomplete (a key was never set)    */
 #define HFG_EIO (-5)       /* HIP runtime error (launch, memcpy, ...)     */
 
-/* Arithmetic of the ResBlock / conv_pre convolutions (the upsamplers, the
- * C<64 stages and conv_post always run the exact fp32 kernels).
+/* Arithmetic of the Generator's convolutions (conv_post + tanh always runs in
+ * exact fp32 on the vector ALUs).
  *   FP32   : fp32 operands on the fp32 matrix cores (v_mfma_f32_32x32x2_f32),
- *            exact fp32 products (the parity reference mode).
+ *            exact fp32 products (the parity reference mode), every conv.
  *   BF16X3 : every fp32 operand split as hi = bf16(v), lo = bf16(v - hi);
  *            hi*hi + hi*lo + lo*hi accumulated in fp32 on the bf16 matrix cores
- *            (~16-bit-mantissa products, 5.3x the fp32 MFMA rate).  Output
- *            within ~1e-6 of the reference, inside the 1e-4 parity bar. */
+ *            (~16-bit-mantissa products, 5.3x the fp32 MFMA rate): conv_pre, the
+ *            upsamplers and every ResBlock conv whose GEMM has >= 32 rows and whose
+ *            (k-1)*dilation fits the kernels' window; the rest (e.g. the 16- and
+ *            8-channel stages of narrow configs) on the fp32 kernels.  Output
+ *            within ~1e-5 of the reference at default weight scale (1e-4 bar). */
 #define HFG_DTYPE_FP32 0
 #define HFG_DTYPE_BF16X3 1
 
@@ -148,6 +157,39 @@ typedef struct hfg_forward_opts {
 int hfg_forward_ex(hfg_handle* h, const float* mel, int64_t B, int64_t T,
                    const hfg_forward_opts* opts, float* wav, int64_t out_len,
                    void* workspace, size_t workspace_bytes, void* stream);
+
+/* ---------------------------------------------------------------------------
+ * One MRF (models/hifigan.py:89-131) as its own handle: the parameters are the
+ * MRF module's state_dict keys "resblocks.{j}.convs{1,2}.{m}.{weight,bias}"
+ * (hfg_set_weight / hfg_commit_weights / hfg_destroy as for a Generator).
+ *   hfg_mrf_forward:      y = MRF.forward(x)      = mean_j ResBlock_j(x)
+ *   hfg_resblock_forward: y = ResBlock_j.forward(x) (all its dilation pairs)
+ * x, y: device fp32 [B][channels][L] (y must not alias x); workspace of
+ * >= hfg_mrf_workspace_bytes(h, B, L) device bytes; async on `stream`.
+ * ------------------------------------------------------------------------- */
+typedef struct hfg_mrf_config {
+    int32_t channels;
+    int32_t n_res;
+    int32_t res_kernels[HFG_MAX_RES];
+    int32_t n_dil[HFG_MAX_RES];
+    int32_t dil[HFG_MAX_RES][HFG_MAX_DIL];
+    int32_t dtype;                               /* HFG_DTYPE_*               */
+} hfg_mrf_config;
+
+int hfg_mrf_create(const hfg_mrf_config* cfg, int device, hfg_handle** out);
+size_t hfg_mrf_workspace_bytes(const hfg_handle* h, int64_t B, int64_t L);
+int hfg_mrf_forward(hfg_handle* h, const float* x, int64_t B, int64_t L, float* y,
+                    void* workspace, size_t workspace_bytes, void* stream);
+int hfg_resblock_forward(hfg_handle* h, int j, const float* x, int64_t B, int64_t L,
+                         float* y, void* workspace, size_t workspace_bytes,
+                         void* stream);
+
+/* Content hash of n device tensors: out[i] (device uint32) = an order-independent
+ * 32-bit hash of the nbytes[i] bytes at ptrs[i] (a multiple of 4).  Async on
+ * `stream`.  The drop-in module compares it with the hash at its last weight
+ * commit to notice edits that bypass autograd's version counter (param.data). */
+int hfg_checksum32(const void* const* ptrs, const int64_t* nbytes, int n,
+                   uint32_t* out, void* stream);
 
 /* Per-launch profiling with HIP events recorded on the launch stream.
  * While enabled, every kernel launch of hfg_forward* is bracketed by an

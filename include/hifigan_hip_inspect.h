@@ -33,6 +33,15 @@ int hfg_debug_packed_layer(hfg_handle* h, const char* mod, float* out, size_t ca
 int hfg_debug_packed_resblock(hfg_handle* h, int stage, int j, float* out, size_t cap,
                               int64_t* info);
 
+/* A Generator forward (one stream) that also copies the stage outputs the
+ * reference's forward passes through (models/hifigan.py:238-251) into
+ * caller-owned device buffers: taps[0] <- conv_pre [B][C0][T], taps[1 + 2i] <-
+ * ups[i] [B][C_i+1][L_i+1], taps[2 + 2i] <- mrfs[i] [B][C_i+1][L_i+1].
+ * n_taps must be 1 + 2 * n_up; NULL entries are skipped. */
+int hfg_forward_taps(hfg_handle* h, const float* mel, int64_t B, int64_t T, float* wav,
+                     int64_t out_len, void* workspace, size_t workspace_bytes,
+                     float* const* taps, int n_taps, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

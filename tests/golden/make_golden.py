@@ -42,6 +42,9 @@ CASES = [
     ("g6_v1_loud2x_b1_t24", "v1", (1, 24), 6, 2.0, False),
     ("g7_v1_b3_t1", "v1", (3, 1), 7, 1.0, False),
     ("g8_v2star_b1_t3", "v2star", (1, 3), 8, 1.0, False),
+    # SURVEY.md §8(c) G6 "loud" at the specified x4 weight scale (tanh far from linear)
+    ("g9_v1_loud4x_b1_t24", "v1", (1, 24), 9, 4.0, False),
+    ("g10_v2star_loud4x_b1_t40", "v2star", (1, 40), 10, 4.0, False),
 ]
 
 FULL_LIMIT = 64 * 1024

@@ -1,0 +1,110 @@
+"""Drop-in boundary on the CPU container (no GPU calls): configuration errors are
+refused at handle creation with the reference's failure modes, the MRF / ResBlock
+handles (hfg_mrf_create) take the MRF module's own state_dict keys, and the
+package imports under its underscore name."""
+import ctypes
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import ROOT
+from oracle import config as C
+
+
+def _create(pkg, **kw):
+    cfg = C.V1.kwargs()
+    cfg.update(kw)
+    c = pkg.make_config(**cfg)
+    lib = pkg.load_library()
+    h = ctypes.c_void_p()
+    rc = lib.hfg_create(ctypes.byref(c), -1, ctypes.byref(h))
+    if rc == 0:
+        lib.hfg_destroy(h)
+    return rc, lib.hfg_last_error().decode()
+
+
+def test_even_resblock_kernel_refused(pkg):
+    # reference: convs2 with get_padding(4, 1) = 1 shortens T by one and x + xt raises
+    rc, msg = _create(pkg, resblock_kernel_sizes=[3, 4, 11])
+    assert rc == -22 and "even kernel" in msg
+
+
+def test_negative_upsample_padding_refused(pkg):
+    # reference: ConvTranspose1d(padding=(k-u)//2 < 0) raises "negative padding is not supported"
+    rc, msg = _create(pkg, upsample_kernel_sizes=[16, 16, 4, 1])
+    assert rc == -22 and "negative padding" in msg
+
+
+def test_unsupported_dilation_refused_at_create(pkg):
+    # (k-1)*d beyond every kernel's staging window: refused before any launch
+    rc, msg = _create(pkg, resblock_dilation_sizes=[[1, 3, 5], [1, 3, 5], [1, 3, 40]])
+    assert rc == -22 and "dilation" in msg
+    rc, _ = _create(pkg, resblock_dilation_sizes=[[1, 3, 5], [1, 3, 5], [1, 3, 12]])
+    assert rc == 0
+
+
+def test_wide_final_stage_accepted(pkg):
+    # conv_post stages its input 32 channels at a time: a 2-stage config ending at
+    # 256 channels (upsample_initial_channel 1024) is valid
+    rc, msg = _create(pkg, upsample_rates=[16, 16], upsample_kernel_sizes=[32, 32],
+                      upsample_initial_channel=1024)
+    assert rc == 0, msg
+
+
+def _mrf_handle(pkg, ch, ks, ds, precision="fp32"):
+    return pkg._lib.Handle(pkg._lib.make_mrf_config(ch, ks, ds, precision), -1, mrf=True)
+
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16x3"])
+def test_mrf_handle_keys_and_commit(pkg, precision):
+    lib = pkg.load_library()
+    mrf = pkg.MRF(64)
+    h = _mrf_handle(pkg, 64, [3, 7, 11], [[1, 3, 5]] * 3, precision)
+    assert lib.hfg_num_params(h.ptr) == len(mrf.state_dict()) == 36
+    with pytest.raises(pkg.HfgError):
+        h.commit()  # nothing set
+    for k, v in mrf.state_dict().items():
+        h.set_weight(k, v)
+    h.commit()
+    assert h.mrf_workspace_bytes(2, 100) >= 2 * 4 * 2 * 64 * 100
+    # generator entry points refuse an MRF handle, MRF entry points a host-only one
+    assert lib.hfg_forward(h.ptr, None, 1, 4, None, 1024, None) == -22
+    assert lib.hfg_out_len(h.ptr, 10) == -1
+    assert lib.hfg_mrf_forward(h.ptr, ctypes.c_void_p(16), 1, 4, ctypes.c_void_p(32),
+                               ctypes.c_void_p(64), 1 << 20, None) == -22
+    assert b"host-only" in lib.hfg_last_error()
+    assert lib.hfg_resblock_forward(h.ptr, 3, ctypes.c_void_p(16), 1, 4, ctypes.c_void_p(32),
+                                    ctypes.c_void_p(64), 1 << 20, None) == -22
+
+
+def test_resblock_module_key_space(pkg):
+    rb = pkg.ResBlock(16, 5, (1, 2))
+    keys = [k for k, _ in rb._hip_weight_items()]
+    assert keys == ["resblocks.0." + k for k in rb.state_dict()]
+    h = _mrf_handle(pkg, 16, [5], [[1, 2]])
+    for k, t in rb._hip_weight_items():
+        h.set_weight(k, t)
+    h.commit()
+
+
+def test_generator_submodules_share_reference_keys(pkg):
+    gen = pkg.HiFiGANGenerator(**C.V2STAR.kwargs())
+    ref_keys = [k for k, _, _ in C.param_specs(C.V2STAR)]
+    assert list(gen.state_dict().keys()) == ref_keys
+    assert list(gen.mrfs[1].state_dict().keys()) == [
+        k[len("mrfs.1."):] for k in ref_keys if k.startswith("mrfs.1.")]
+    gen.set_precision("bf16x3")
+    assert {m.precision for m in gen.modules() if hasattr(m, "precision")} == {"bf16x3"}
+
+
+def test_package_imports_by_underscore_name():
+    code = ("import tts_sambert_hifigan_amd as p, tts_sambert_hifigan_amd.glue as g; "
+            "print(p.HiFiGANGenerator.__module__, os.path.basename(os.path.dirname(g.__file__)))")
+    out = subprocess.run([sys.executable, "-c", "import os; " + code], cwd=ROOT,
+                         capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr
+    assert out.stdout.split() == ["tts_sambert_hifigan_amd.hifigan", "tts-sambert_hifigan_amd"]

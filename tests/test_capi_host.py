@@ -24,14 +24,14 @@ def header_symbols():
     for h in ("hifigan_hip.h", "hifigan_hip_inspect.h"):
         src = open(os.path.join(ROOT, "include", h)).read()
         src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
-        syms |= set(re.findall(r"\b(hfg_[a-z_]+)\s*\(", src))
+        syms |= set(re.findall(r"\b(hfg_[a-z0-9_]+)\s*\(", src))
     return syms
 
 
 def test_library_exports_every_header_symbol(pkg):
     lib = pkg.load_library()
     syms = header_symbols()
-    assert len(syms) == 26
+    assert len(syms) == 32
     for s in sorted(syms):
         assert hasattr(lib, s), f"missing export {s}"
     assert set(syms) == set(pkg._lib.SIGNATURES), "ctypes signatures out of sync with headers"

@@ -1,0 +1,138 @@
+"""The BASELINE.json workloads on the GPU, each at its own size (configs 3, 4, 5;
+config 2 is covered by test_gpu_properties.py).
+
+* C4  V2* [16, 80, 2048] (SURVEY.md §8(a) pinned V2*): receptive-field windows of
+      several utterances (head, middle, end) against the oracle, and batch-split
+      bitwise invariance.
+* C3  V1 [64, 80, 1024] on one GPU: the whole 8-GPU batch in one forward; windows
+      against the oracle, and each [8, 80, 1024] shard (one rank's workload) bitwise
+      equal to the corresponding rows of the full batch.
+* C5  SAM-BERT acoustic model -> mel -> vocoder, batch 32 ragged: the reference
+      acoustic model's output (tests/golden/c5_sambert_b32.npz, make_c5_golden.py)
+      vocoded through hfg_forward_ex ([B, T, 80] layout, per-utterance lengths) and
+      compared with the reference Generator's wav (fixture) and the oracle.
+Tolerance: fp32 atol 1e-4 on the wav (north_star), both precisions.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN_DIR
+
+pytestmark = pytest.mark.gpu
+ATOL = 1e-4
+
+
+@pytest.fixture(scope="module")
+def dev():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    return torch.device("cuda:0")
+
+
+def _gen(pkg, cfg, sd, dev, precision):
+    gen = pkg.HiFiGANGenerator(**cfg.kwargs(), precision=precision).eval()
+    gen.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
+    return gen.to(dev)
+
+
+def _run(gen, mel, **kw):
+    with torch.no_grad():
+        out = gen(mel, **kw)
+    torch.cuda.synchronize()
+    return out
+
+
+def _window_check(cfg, sd, mel, wav, item, start, W, M):
+    from oracle import hifigan_torch as H
+    T = mel.shape[-1]
+    hop = wav.shape[-1] // T
+    a, b = max(0, start - M), min(T, start + W + M)
+    ref = H.generator_forward(H.to_torch_state(sd), cfg, mel[item:item + 1, :, a:b])
+    ref = ref[0, 0, (start - a) * hop:(start - a + W) * hop].numpy()
+    got = wav[item, 0, start * hop:(start + W) * hop].cpu().numpy()
+    return float(np.abs(got - ref).max())
+
+
+@pytest.mark.parametrize("precision", ["bf16x3", "fp32"])
+def test_c4_v2star_16x80x2048(pkg, dev, precision):
+    from oracle import config as C
+    cfg = C.V2STAR
+    sd = C.make_state_dict(cfg, seed=4)
+    gen = _gen(pkg, cfg, sd, dev, precision)
+    M = gen.receptive_field_frames() + 1
+    g = torch.Generator().manual_seed(1234)
+    mel = torch.randn(16, 80, 2048, generator=g)
+    wav = _run(gen, mel.to(dev))
+    assert wav.shape == (16, 1, 2048 * 256)
+    errs = [_window_check(cfg, sd, mel, wav, item, start, 40, M)
+            for item, start in [(0, 0), (5, 1000), (11, 2048 - 40), (15, 517)]]
+    print(f"\nC4 [{precision}] window errors {['%.2e' % e for e in errs]}")
+    assert max(errs) < ATOL
+    for lo, hi in [(3, 4), (8, 13)]:
+        part = _run(gen, mel[lo:hi].to(dev))
+        assert torch.equal(part, wav[lo:hi]), (lo, hi)
+
+
+@pytest.mark.parametrize("precision", ["bf16x3", "fp32"])
+def test_c3_v1_64x80x1024_one_gpu(pkg, dev, precision):
+    from oracle import config as C
+    cfg = C.V1
+    sd = C.make_state_dict(cfg, seed=3)
+    gen = _gen(pkg, cfg, sd, dev, precision)
+    g = torch.Generator().manual_seed(1234)
+    mel = torch.randn(64, 80, 1024, generator=g)
+    wav = _run(gen, mel.to(dev))
+    assert wav.shape == (64, 1, 1024 * 256)
+    errs = [_window_check(cfg, sd, mel, wav, item, start, 32, 16)
+            for item, start in [(0, 0), (33, 600), (63, 1024 - 32)]]
+    print(f"\nC3 [{precision}] window errors {['%.2e' % e for e in errs]}")
+    assert max(errs) < ATOL
+    for r in (0, 3, 7):  # rank r's shard of the 8-GPU run
+        shard = _run(gen, mel[8 * r:8 * r + 8].to(dev))
+        assert torch.equal(shard, wav[8 * r:8 * r + 8]), r
+    del wav
+    torch.cuda.empty_cache()
+
+
+@pytest.fixture(scope="module")
+def c5():
+    meta = json.load(open(os.path.join(GOLDEN_DIR, "golden_c5.json")))
+    d = np.load(os.path.join(GOLDEN_DIR, "c5_sambert_b32.npz"))
+    return meta, {k: d[k] for k in d.files}
+
+
+@pytest.mark.parametrize("precision", ["bf16x3", "fp32"])
+def test_c5_sambert_batch32_ragged(pkg, dev, c5, precision):
+    import importlib
+    from oracle import config as C, hifigan_torch as H
+    glue = importlib.import_module("tts_sambert_hifigan_amd.glue")
+    meta, arr = c5
+    cfg = C.V1
+    sd = C.make_state_dict(cfg, seed=meta["vocoder_seed"])
+    gen = _gen(pkg, cfg, sd, dev, precision)
+    mel_pred = torch.from_numpy(arr["mel_pred"])  # [32, T, 80] as the acoustic model emits it
+    lens = [int(x) for x in arr["lengths"]]
+    assert mel_pred.shape[0] == 32 and max(lens) == mel_pred.shape[1]
+    wavs = glue.vocode_acoustic(gen, mel_pred.to(dev), lens)
+    torch.cuda.synchronize()
+    tsd = H.to_torch_state(sd)
+    worst = 0.0
+    for b in range(32):
+        w = wavs[b].cpu().numpy()
+        st = meta["wav"][str(b)]
+        assert list(w.shape) == st["shape"], b
+        l2 = float(np.sqrt((w.astype(np.float64) ** 2).sum()))
+        assert abs(l2 - st["l2"]) <= 1e-3 * st["l2"], b
+        if b in meta["full_wav"]:
+            err = float(np.abs(w - arr[f"wav_{b}"]).max())  # the reference Generator's wav
+            worst = max(worst, err)
+            assert err < ATOL, (b, err)
+        ref = H.generator_forward(tsd, cfg, mel_pred[b:b + 1, :lens[b]].transpose(1, 2))
+        err = float(np.abs(w - ref[0, 0].numpy()).max())
+        worst = max(worst, err)
+        assert err < ATOL, (b, err)
+    print(f"\nC5 [{precision}] 32 utterances, frames {min(lens)}-{max(lens)}: max err {worst:.2e}")

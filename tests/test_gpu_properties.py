@@ -294,3 +294,63 @@ def test_over_max_length_rejected(pkg, v1, dev):
                             256, None)
     assert rc == -22
     assert b"exceeds 2^30" in lib.hfg_last_error()
+
+
+# ---- weight tracking and 2-stream capture -------------------------------------------
+def test_weight_edit_through_data_is_picked_up(pkg, dev):
+    """An in-place edit through ``param.data`` leaves autograd's version counter alone;
+    the module's content hash (hfg_checksum32) still notices it, so the next forward
+    runs on the new weights.  Same for a ResBlock on its own."""
+    from oracle import config as C, hifigan_torch as H, prng
+    cfg = C.V2STAR
+    sd = C.make_state_dict(cfg, seed=8)
+    gen = pkg.HiFiGANGenerator(**cfg.kwargs()).eval()
+    gen.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
+    gen = gen.to(dev)
+    mel = torch.from_numpy(prng.mel_input(8, (1, 80, 20))).to(dev)
+    w0 = run(gen, mel).clone()
+    v0 = gen.ups[1].weight._version
+    gen.ups[1].weight.data.mul_(1.5)
+    gen.mrfs[2].resblocks[0].convs2[1].bias.data.add_(0.01)
+    assert gen.ups[1].weight._version == v0
+    w1 = run(gen, mel)
+    assert not torch.equal(w0, w1)
+    sd2 = {k: v.detach().cpu() for k, v in gen.state_dict().items()}
+    ref = H.generator_forward(sd2, cfg, mel.cpu())
+    assert (w1.cpu() - ref).abs().max().item() < ATOL
+    rb = gen.mrfs[0].resblocks[1]
+    x = torch.randn(2, rb.channels, 50, device=dev)
+    y0 = run(rb, x).clone()
+    rb.convs1[0].weight.data.neg_()
+    assert not torch.equal(y0, run(rb, x))
+    # with verification off, refresh_weights() is the explicit route
+    gen.verify_weights = False
+    gen.ups[1].weight.data.mul_(1 / 1.5)
+    assert torch.equal(run(gen, mel), w1)
+    gen.refresh_weights()
+    assert not torch.equal(run(gen, mel), w1)
+
+
+def test_hipgraph_capture_two_stream_forward(v1, dev):
+    """A forward big enough for the two-stream batch split (B x T >= 4096 frames: the
+    caller's stream forks to the handle's internal stream and joins back) is captured
+    into a hipGraph and replays to the eager result."""
+    gen, _ = v1
+    h = gen.hip_handle(dev)
+    h.set_streams(2)
+    mel = torch.randn(4, 80, 1100, device=dev)
+    with torch.no_grad():
+        s = torch.cuda.Stream(dev)
+        s.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(s):
+            gen(mel)
+        torch.cuda.current_stream(dev).wait_stream(s)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            out = gen(mel)
+        mel.copy_(torch.randn(4, 80, 1100, device=dev))
+        g.replay()
+        torch.cuda.synchronize()
+        ref = gen(mel)
+    torch.cuda.synchronize()
+    assert torch.equal(out, ref)

@@ -63,6 +63,40 @@ class HfgConfig(ctypes.Structure):
 DTYPES = {"fp32": 0, "bf16x3": 1}
 
 
+class HfgMrfConfig(ctypes.Structure):
+    _fields_ = [
+        ("channels", c_int32),
+        ("n_res", c_int32),
+        ("res_kernels", c_int32 * HFG_MAX_RES),
+        ("n_dil", c_int32 * HFG_MAX_RES),
+        ("dil", (c_int32 * HFG_MAX_DIL) * HFG_MAX_RES),
+        ("dtype", c_int32),
+    ]
+
+
+def make_mrf_config(channels, resblock_kernel_sizes, resblock_dilation_sizes,
+                    precision: str = "fp32") -> HfgMrfConfig:
+    """One MRF's hyper-parameters (MRF.__init__, models/hifigan.py:96-114)."""
+    n = min(len(resblock_kernel_sizes), len(resblock_dilation_sizes))  # zip semantics
+    if n > HFG_MAX_RES:
+        raise ValueError("too many resblocks for the ABI")
+    c = HfgMrfConfig()
+    c.channels = int(channels)
+    c.n_res = n
+    for j in range(n):
+        dils = list(resblock_dilation_sizes[j])
+        if len(dils) > HFG_MAX_DIL:
+            raise ValueError("too many dilations in one ResBlock")
+        c.res_kernels[j] = int(resblock_kernel_sizes[j])
+        c.n_dil[j] = len(dils)
+        for m, d in enumerate(dils):
+            c.dil[j][m] = int(d)
+    if precision not in DTYPES:
+        raise ValueError(f"precision must be one of {sorted(DTYPES)}")
+    c.dtype = DTYPES[precision]
+    return c
+
+
 def make_config(n_mels, upsample_rates, upsample_kernel_sizes, upsample_initial_channel,
                 resblock_kernel_sizes, resblock_dilation_sizes, precision: str = "fp32") -> HfgConfig:
     if len(upsample_rates) != len(upsample_kernel_sizes):
@@ -129,6 +163,15 @@ SIGNATURES = {
                                        POINTER(c_int64)]),
     "hfg_debug_packed_resblock": (c_int, [c_void_p, c_int, c_int, POINTER(c_float), c_size_t,
                                           POINTER(c_int64)]),
+    "hfg_mrf_create": (c_int, [POINTER(HfgMrfConfig), c_int, POINTER(c_void_p)]),
+    "hfg_mrf_workspace_bytes": (c_size_t, [c_void_p, c_int64, c_int64]),
+    "hfg_mrf_forward": (c_int, [c_void_p, c_void_p, c_int64, c_int64, c_void_p, c_void_p,
+                                c_size_t, c_void_p]),
+    "hfg_resblock_forward": (c_int, [c_void_p, c_int, c_void_p, c_int64, c_int64, c_void_p,
+                                     c_void_p, c_size_t, c_void_p]),
+    "hfg_checksum32": (c_int, [POINTER(c_void_p), POINTER(c_int64), c_int, c_void_p, c_void_p]),
+    "hfg_forward_taps": (c_int, [c_void_p, c_void_p, c_int64, c_int64, c_void_p, c_int64,
+                                 c_void_p, c_size_t, POINTER(c_void_p), c_int, c_void_p]),
     "hfg_mel_last_error": (c_char_p, []),
     "hfg_mel_create": (c_int, [POINTER(HfgMelConfig), c_int, POINTER(c_void_p)]),
     "hfg_mel_destroy": (None, [c_void_p]),
@@ -165,14 +208,33 @@ def check(rc: int):
     return rc
 
 
-class Handle:
-    """Owning wrapper of an ``hfg_handle*`` (one per device)."""
+def checksum32(tensors) -> "torch.Tensor":
+    """Content hash per fp32 device tensor (hfg_checksum32) as an int64 CPU tensor.
+    Synchronises with the current stream (the result is copied to the host)."""
+    if not tensors:
+        return torch.zeros(0, dtype=torch.int64)
+    lib = load_library()
+    dev = tensors[0].device
+    n = len(tensors)
+    out = torch.empty(n, dtype=torch.int32, device=dev)
+    ptrs = (c_void_p * n)(*[t.data_ptr() for t in tensors])
+    nbytes = (c_int64 * n)(*[t.numel() * t.element_size() for t in tensors])
+    check(lib.hfg_checksum32(ptrs, nbytes, n, c_void_p(out.data_ptr()),
+                             c_void_p(torch.cuda.current_stream(dev).cuda_stream)))
+    return out.cpu().to(torch.int64)
 
-    def __init__(self, cfg: HfgConfig, device: int):
+
+class Handle:
+    """Owning wrapper of an ``hfg_handle*`` (one per device): a Generator handle
+    (``hfg_create``) or, with ``mrf=True``, an MRF handle (``hfg_mrf_create``)."""
+
+    def __init__(self, cfg, device: int, mrf: bool = False):
         self.lib = load_library()
         self.device = device
+        self.mrf = mrf
         h = c_void_p()
-        check(self.lib.hfg_create(ctypes.byref(cfg), int(device), ctypes.byref(h)))
+        create = self.lib.hfg_mrf_create if mrf else self.lib.hfg_create
+        check(create(ctypes.byref(cfg), int(device), ctypes.byref(h)))
         self.ptr = h
 
     def __del__(self):
@@ -184,9 +246,14 @@ class Handle:
             pass
 
     def set_weight(self, name: str, t: "torch.Tensor"):
+        """Copy one parameter in (hfg_set_weight).  A device tensor is first ordered
+        after the producing work on torch's current stream (the library's D2H copy
+        runs on the null stream)."""
         t = t.detach()
         is_dev = 1 if t.is_cuda else 0
         t = t.to(torch.float32).contiguous()
+        if is_dev:
+            torch.cuda.current_stream(t.device).synchronize()
         shape = (c_int64 * max(t.dim(), 1))(*t.shape)
         check(self.lib.hfg_set_weight(self.ptr, name.encode(), c_void_p(t.data_ptr()), shape,
                                       t.dim(), is_dev))
@@ -212,6 +279,28 @@ class Handle:
         check(self.lib.hfg_forward_ex(self.ptr, c_void_p(mel_ptr), int(B), int(T), ctypes.byref(o),
                                       c_void_p(wav_ptr), int(out_len), c_void_p(ws_ptr),
                                       int(ws_bytes), c_void_p(stream)))
+
+    def forward_taps(self, mel_ptr: int, B: int, T: int, wav_ptr: int, out_len: int, ws_ptr: int,
+                     ws_bytes: int, tap_ptrs, stream: int):
+        n = len(tap_ptrs)
+        arr = (c_void_p * n)(*[p if p else None for p in tap_ptrs])
+        check(self.lib.hfg_forward_taps(self.ptr, c_void_p(mel_ptr), int(B), int(T),
+                                        c_void_p(wav_ptr), int(out_len), c_void_p(ws_ptr),
+                                        int(ws_bytes), arr, n, c_void_p(stream)))
+
+    def mrf_workspace_bytes(self, B: int, L: int) -> int:
+        return int(self.lib.hfg_mrf_workspace_bytes(self.ptr, int(B), int(L)))
+
+    def mrf_forward(self, x_ptr: int, B: int, L: int, y_ptr: int, ws_ptr: int, ws_bytes: int,
+                    stream: int, resblock: int = -1):
+        if resblock < 0:
+            check(self.lib.hfg_mrf_forward(self.ptr, c_void_p(x_ptr), int(B), int(L),
+                                           c_void_p(y_ptr), c_void_p(ws_ptr), int(ws_bytes),
+                                           c_void_p(stream)))
+        else:
+            check(self.lib.hfg_resblock_forward(self.ptr, int(resblock), c_void_p(x_ptr), int(B),
+                                                int(L), c_void_p(y_ptr), c_void_p(ws_ptr),
+                                                int(ws_bytes), c_void_p(stream)))
 
     def set_streams(self, n: int):
         """1: every launch on the caller's stream; 2: batch halves on two streams."""

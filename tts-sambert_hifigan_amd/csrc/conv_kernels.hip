@@ -226,17 +226,19 @@ conv1d_mfma_f32(const ConvParams p) {
   }
 }
 
-// conv_post (C -> 1, k=7, pad=3) + tanh over lrelu(x).  One thread per sample,
-// a 256-sample tile of all C input rows staged in LDS.
+// conv_post (C -> 1, k=7, pad=3) + tanh over lrelu(x).  One thread per sample; the
+// 256-sample tile's input rows are staged in LDS kConvPostCB channels at a time (the
+// halo columns are shared between neighbouring threads), so any channel count fits.
 __global__ void __launch_bounds__(256)
 conv_post_tanh(const float* __restrict__ x, int64_t x_bs, int C, int L, const float* __restrict__ w,
                const float* __restrict__ bias, float* __restrict__ wav,
                const int32_t* __restrict__ lens) {
   constexpr int TT = 256, KP = 7, HALO = 3;
   constexpr int XW = TT + KP - 1;
+  constexpr int CBLK = kConvPostCB;
   extern __shared__ __attribute__((aligned(16))) float lds[];
   float* Ws = lds;              // C*7
-  float* Xs = lds + ((C * KP + 3) & ~3);  // C*XW
+  float* Xs = lds + ((C * KP + 3) & ~3);  // CBLK*XW
   const int t0 = blockIdx.x * TT;
   const int b = blockIdx.y;
   const float* xb = x + (int64_t)b * x_bs;
@@ -256,36 +258,36 @@ conv_post_tanh(const float* __restrict__ x, int64_t x_bs, int C, int L, const fl
   const int gh = t0 - HALO + TT + tt;  // halo column (tt < KP - 1), always >= 0
   const bool okm = gm >= 0 && gm < Lb;
   const bool okh = tt < KP - 1 && gh < Lb;
-  for (int c0 = 0; c0 < C; c0 += CB) {
-    float vm[CB], vh[CB];
+  float acc = 0.f;
+  for (int cb = 0; cb < C; cb += CBLK) {
+    const int nc = min(CBLK, C - cb);
+    if (cb > 0) __syncthreads();  // the previous block's rows are consumed
+    for (int c0 = 0; c0 < nc; c0 += CB) {
+      float vm[CB], vh[CB];
 #pragma unroll
-    for (int e = 0; e < CB; ++e) {
-      const int64_t row = (int64_t)min(c0 + e, C - 1) * L;
-      vm[e] = xb[okm ? row + gm : 0];
-      vh[e] = xb[okh ? row + gh : 0];
+      for (int e = 0; e < CB; ++e) {
+        const int64_t row = (int64_t)(cb + min(c0 + e, nc - 1)) * L;
+        vm[e] = xb[okm ? row + gm : 0];
+        vh[e] = xb[okh ? row + gh : 0];
+      }
+#pragma unroll
+      for (int e = 0; e < CB; ++e) {
+        if (c0 + e >= nc) break;
+        Xs[(c0 + e) * XW + tt] = okm ? lrelu(vm[e]) : 0.f;
+        if (tt < KP - 1) Xs[(c0 + e) * XW + TT + tt] = okh ? lrelu(vh[e]) : 0.f;
+      }
     }
+    __syncthreads();
+    for (int c = 0; c < nc; ++c) {
+      const float* xs = Xs + c * XW + threadIdx.x;
+      const float* ws = Ws + (cb + c) * KP;
 #pragma unroll
-    for (int e = 0; e < CB; ++e) {
-      if (c0 + e >= C) break;
-      Xs[(c0 + e) * XW + tt] = okm ? lrelu(vm[e]) : 0.f;
-      if (tt < KP - 1) Xs[(c0 + e) * XW + TT + tt] = okh ? lrelu(vh[e]) : 0.f;
+      for (int j = 0; j < KP; ++j) acc = fmaf(ws[j], xs[j], acc);
     }
   }
-  __syncthreads();
   const int t = t0 + threadIdx.x;
   if (t >= L) return;
-  if (t >= Lb) {
-    wav[(int64_t)b * L + t] = 0.f;
-    return;
-  }
-  float acc = 0.f;
-  for (int c = 0; c < C; ++c) {
-    const float* xs = Xs + c * XW + threadIdx.x;
-    const float* ws = Ws + c * KP;
-#pragma unroll
-    for (int j = 0; j < KP; ++j) acc = fmaf(ws[j], xs[j], acc);
-  }
-  wav[(int64_t)b * L + t] = tanhf(acc + bias[0]);
+  wav[(int64_t)b * L + t] = t >= Lb ? 0.f : tanhf(acc + bias[0]);
 }
 
 // ------------------------------------------------------------------------
@@ -362,7 +364,7 @@ hipError_t launch_conv(TileId tile, int kt, bool ups, const ConvParams& p, int n
 hipError_t launch_conv_post(const float* x, int64_t x_bs, int C, int L, const float* w,
                             const float* bias, float* wav, const int32_t* lens, int batch,
                             hipStream_t stream, const char** name) {
-  const size_t lds = sizeof(float) * ((size_t)((C * 7 + 3) & ~3) + (size_t)C * (256 + 6));
+  const size_t lds = conv_post_lds_bytes(C);
   if (lds > 160 * 1024) return hipErrorInvalidValue;
   static bool attr = false;
   if (lds > 64 * 1024 && !attr) {
@@ -396,6 +398,48 @@ __global__ void stage_lengths_kernel(const int32_t* __restrict__ lens, int B, St
 hipError_t launch_stage_lengths(const int32_t* lens, int B, const StageLenParams& sp,
                                 int32_t* out, hipStream_t stream) {
   stage_lengths_kernel<<<dim3((B + 255) / 256), dim3(256), 0, stream>>>(lens, B, sp, out);
+  return hipGetLastError();
+}
+
+bool fp32_conv_supported(int tile, int kt, int dil) {
+  const int dkt = dispatch_kt(kt);
+  if (kt < 1 || dil < 1 || (kt - 1) * dil > halo_max(dkt)) return false;
+  const TileCfg& t = kTiles[tile];
+  const int ck = ck_for(dkt, tile);
+  const int xw = t.NTILE() + (kt - 1) * dil;
+  const size_t stage = (size_t)t.MT() * ck * kt + (((size_t)ck * xw + 3) & ~(size_t)3);
+  return sizeof(float) * 2 * stage <= 160 * 1024;
+}
+
+// Order-independent 32-bit content hash of fp32 tensors (the drop-in module's check that
+// its parameters did not change behind its back, e.g. through ``param.data``): every
+// word is mixed with its index and the mixes are summed mod 2^32 (vector atomics).
+__device__ __forceinline__ uint32_t ck_mix(uint32_t w, uint32_t i) {
+  uint32_t h = w * 0x9E3779B1u ^ (i * 0x85EBCA77u + 0x165667B1u);
+  h ^= h >> 15;
+  h *= 0xC2B2AE3Du;
+  h ^= h >> 13;
+  return h;
+}
+
+__global__ void __launch_bounds__(256) checksum_kernel(ChecksumArgs a, uint32_t* __restrict__ out) {
+  const int t = blockIdx.y;
+  const uint32_t* p = a.p[t];
+  const int64_t n = a.n[t];
+  uint32_t acc = 0;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
+    acc += ck_mix(p[i], (uint32_t)i);
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) acc += __shfl_xor(acc, o, 64);
+  if ((threadIdx.x & 63) == 0) atomicAdd(out + a.base + t, acc);
+}
+
+hipError_t launch_checksum(const ChecksumArgs& a, uint32_t* out, hipStream_t stream) {
+  int64_t mx = 1;
+  for (int i = 0; i < a.count; ++i) mx = a.n[i] > mx ? a.n[i] : mx;
+  const int64_t want = (mx + 256 * 8 - 1) / (256 * 8);
+  const int gx = (int)(want < 512 ? want : 512);
+  checksum_kernel<<<dim3(gx, a.count), dim3(256), 0, stream>>>(a, out);
   return hipGetLastError();
 }
 

@@ -12,6 +12,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <map>
+#include <mutex>
 #include <string>
 #include <tuple>
 #include <vector>
@@ -84,7 +85,8 @@ struct RbFused {
 };
 
 struct Stage {
-  int conv_ups;               // index of the ups layer
+  int C = 0;                  // channels of this stage's MRF
+  int conv_ups = -1;          // index of the ups layer (-1 in an MRF-only handle)
   std::vector<int> conv1;     // [j*n_dil + m]
   std::vector<int> conv2;
   std::vector<RbFused> rbs;   // per ResBlock: whole-block launch or layer by layer
@@ -95,6 +97,12 @@ struct Stage {
 struct hfg_handle {
   hfg_config cfg;
   int device;  // -1: host-only handle (validation / packing inspection)
+  // MRF-only handle (hfg_mrf_create): one stage of ResBlocks keyed "resblocks.{j}.*"
+  // (the MRF module's own state_dict), no conv_pre / ups / conv_post
+  bool mrf_only = false;
+  // one forward at a time per handle: the split stream, its fork/join events and the
+  // profiling records are shared state (ctypes releases the GIL around the call)
+  std::recursive_mutex mu;
   std::vector<Layer> layers;
   int conv_pre = -1, conv_post = -1;
   std::vector<Stage> stages;
@@ -157,8 +165,19 @@ int validate_config(const hfg_config* c) {
       return fail(HFG_EINVAL, "upsample rate/kernel %d must be > 0", i);
     if ((c->c0 >> (i + 1)) <= 0) return fail(HFG_EINVAL, "channels vanish at stage %d", i);
   }
+  for (int i = 0; i < c->n_up; ++i)
+    if (c->up_kernels[i] < c->up_rates[i])
+      // ConvTranspose1d(padding=(k-u)//2 < 0): torch raises "negative padding is not supported"
+      return fail(HFG_EINVAL, "ups.%d: kernel %d < stride %d gives negative padding (k-u)//2; "
+                  "negative padding is not supported", i, c->up_kernels[i], c->up_rates[i]);
   for (int j = 0; j < c->n_res; ++j) {
     if (c->res_kernels[j] <= 0) return fail(HFG_EINVAL, "resblock kernel %d must be > 0", j);
+    if (c->res_kernels[j] % 2 == 0)
+      // convs2 (dilation 1, padding get_padding(k, 1) = (k-1)//2) shortens the sequence by
+      // one, so the reference's residual add x + xt (models/hifigan.py:85) fails
+      return fail(HFG_EINVAL, "resblock %d: even kernel size %d is not length-preserving "
+                  "(the reference's residual add x + xt fails on the size mismatch)", j,
+                  c->res_kernels[j]);
     if (c->n_dil[j] <= 0 || c->n_dil[j] > HFG_MAX_DIL)
       return fail(HFG_EINVAL, "resblock %d dilation count out of range", j);
     for (int m = 0; m < c->n_dil[j]; ++m)
@@ -192,48 +211,62 @@ int add_conv(hfg_handle* h, LayerKind kind, const std::string& mod, int cin, int
   return (int)h->layers.size() - 1;
 }
 
-// Build the layer list in the order of HiFiGANGenerator.__init__ (models/hifigan.py:177-222).
-void build_layers(hfg_handle* h) {
+// The ResBlock convs of one MRF (models/hifigan.py:96-114 / ResBlock.__init__ :34-70),
+// state_dict keys "<pre>resblocks.{j}.convs{1,2}.{m}".
+Stage build_stage(hfg_handle* h, int ch, const std::string& pre) {
   const hfg_config& c = h->cfg;
-  h->conv_pre = add_conv(h, L_CONV, "conv_pre", c.n_mels, c.c0, 7, 1, 3);
-  std::vector<int> ups_idx;
-  for (int i = 0; i < c.n_up; ++i) {
-    const int cin = c.c0 >> i, cout = c.c0 >> (i + 1);
-    const int u = c.up_rates[i], k = c.up_kernels[i];
-    Layer L{};
-    L.kind = L_UPS;
-    L.mod = "ups." + std::to_string(i);
-    L.C_in = cin;
-    L.C_out = cout;
-    L.k = k;
-    L.dil = 1;
-    L.s = u;
-    L.p = (k - u) / 2;  // models/hifigan.py:201 — Python floor division
-    if (k - u < 0 && (k - u) % 2 != 0) L.p -= 1;
-    L.M = cout * u;
-    L.KT = (k + u - 1) / u;  // taps per output phase
-    h->layers.push_back(L);
-    ups_idx.push_back((int)h->layers.size() - 1);
-    add_param(h, L.mod + ".weight", {cin, cout, k});
-    add_param(h, L.mod + ".bias", {cout});
+  Stage st;
+  st.C = ch;
+  for (int j = 0; j < c.n_res; ++j) {
+    const int kr = c.res_kernels[j];
+    const std::string rb = pre + "resblocks." + std::to_string(j);
+    for (int m = 0; m < c.n_dil[j]; ++m)
+      st.conv1.push_back(add_conv(h, L_CONV, rb + ".convs1." + std::to_string(m), ch, ch, kr,
+                                  c.dil[j][m], get_padding(kr, c.dil[j][m])));
+    for (int m = 0; m < c.n_dil[j]; ++m)
+      st.conv2.push_back(add_conv(h, L_CONV, rb + ".convs2." + std::to_string(m), ch, ch, kr, 1,
+                                  get_padding(kr, 1)));
   }
-  for (int i = 0; i < c.n_up; ++i) {
-    const int ch = c.c0 >> (i + 1);
-    Stage st;
-    st.conv_ups = ups_idx[i];
-    for (int j = 0; j < c.n_res; ++j) {
-      const int kr = c.res_kernels[j];
-      const std::string pre = "mrfs." + std::to_string(i) + ".resblocks." + std::to_string(j);
-      for (int m = 0; m < c.n_dil[j]; ++m)
-        st.conv1.push_back(add_conv(h, L_CONV, pre + ".convs1." + std::to_string(m), ch, ch, kr,
-                                    c.dil[j][m], get_padding(kr, c.dil[j][m])));
-      for (int m = 0; m < c.n_dil[j]; ++m)
-        st.conv2.push_back(add_conv(h, L_CONV, pre + ".convs2." + std::to_string(m), ch, ch, kr, 1,
-                                    get_padding(kr, 1)));
+  return st;
+}
+
+// Build the layer list in the order of HiFiGANGenerator.__init__ (models/hifigan.py:177-222)
+// (an MRF-only handle: the one MRF).  Returns HFG_EINVAL when a layer's taps x dilation is
+// beyond every kernel's staging limits.
+int build_layers(hfg_handle* h) {
+  const hfg_config& c = h->cfg;
+  if (h->mrf_only) {
+    h->stages.push_back(build_stage(h, c.c0 >> 1, ""));
+  } else {
+    h->conv_pre = add_conv(h, L_CONV, "conv_pre", c.n_mels, c.c0, 7, 1, 3);
+    std::vector<int> ups_idx;
+    for (int i = 0; i < c.n_up; ++i) {
+      const int cin = c.c0 >> i, cout = c.c0 >> (i + 1);
+      const int u = c.up_rates[i], k = c.up_kernels[i];
+      Layer L{};
+      L.kind = L_UPS;
+      L.mod = "ups." + std::to_string(i);
+      L.C_in = cin;
+      L.C_out = cout;
+      L.k = k;
+      L.dil = 1;
+      L.s = u;
+      L.p = (k - u) / 2;  // models/hifigan.py:201 — Python floor division
+      if (k - u < 0 && (k - u) % 2 != 0) L.p -= 1;
+      L.M = cout * u;
+      L.KT = (k + u - 1) / u;  // taps per output phase
+      h->layers.push_back(L);
+      ups_idx.push_back((int)h->layers.size() - 1);
+      add_param(h, L.mod + ".weight", {cin, cout, k});
+      add_param(h, L.mod + ".bias", {cout});
     }
-    h->stages.push_back(std::move(st));
+    for (int i = 0; i < c.n_up; ++i) {
+      Stage st = build_stage(h, c.c0 >> (i + 1), "mrfs." + std::to_string(i) + ".");
+      st.conv_ups = ups_idx[i];
+      h->stages.push_back(std::move(st));
+    }
+    h->conv_post = add_conv(h, L_POST, "conv_post", c.c0 >> c.n_up, 1, 7, 1, 3);
   }
-  h->conv_post = add_conv(h, L_POST, "conv_post", c.c0 >> c.n_up, 1, 7, 1, 3);
 
   // GEMM tiling and packed-buffer offsets
   size_t off = 0;
@@ -281,7 +314,7 @@ void build_layers(hfg_handle* h) {
       continue;
     }
     if (h->cfg.dtype == HFG_DTYPE_BF16X3 && (L.kind == L_CONV || L.kind == L_UPS) &&
-        hfg::bf16x3_tile_for_rows(L.M) >= 0 && (L.KT - 1) * L.dil <= hfg::kBf16x3MaxHalo) {
+        hfg::bf16x3_tile_for_rows(L.M) >= 0 && hfg::bf16x3_supported(L.KT, L.dil)) {
       // split-precision path: chunk = 16 channels x TPC taps
       L.tile = hfg::bf16x3_tile_for_rows(L.M, h->big_tile == hfg::kWsTile ? 3 : h->big_tile);
       const hfg::Bf16x3Cfg& t3 = hfg::kBf16x3Tiles[L.tile];
@@ -300,6 +333,10 @@ void build_layers(hfg_handle* h) {
     }
     L.prec = 0;
     L.tile = hfg::tile_for_rows(L.M);
+    if (!hfg::fp32_conv_supported(L.tile, L.KT, L.dil))
+      return fail(HFG_EINVAL, "%s: %d taps at dilation %d span (k-1)*d = %d samples, beyond the "
+                  "conv kernels' staging window (max %d)", L.mod.c_str(), L.KT, L.dil,
+                  (L.KT - 1) * L.dil, hfg::halo_max(hfg::dispatch_kt(L.KT)));
     const TileCfg& t = kTiles[L.tile];
     L.CK = hfg::ck_for(hfg::dispatch_kt(L.KT), L.tile);
     L.m_tiles = (L.M + t.MT() - 1) / t.MT();
@@ -313,9 +350,9 @@ void build_layers(hfg_handle* h) {
   }
   // whole-ResBlock launches (bf16x3 only): every ResBlock of the C in {32, 64} stages, and
   // those of C = 128 whose receptive field costs <= 15% recomputation (k = 3 in V1)
-  for (int i = 0; i < c.n_up; ++i) {
+  for (size_t i = 0; i < h->stages.size(); ++i) {
     Stage& st = h->stages[i];
-    const int C = c.c0 >> (i + 1);
+    const int C = st.C;
     st.rbs.assign(c.n_res, RbFused{});
     if (h->cfg.dtype != HFG_DTYPE_BF16X3 || !h->use_fused_rb || (C != 32 && C != 64 && C != 128))
       continue;
@@ -355,6 +392,7 @@ void build_layers(hfg_handle* h) {
     }
   }
   h->packed_host.assign(off, 0.f);
+  return HFG_OK;
 }
 
 // Fragment order of conv1d_mfma_f32's A operand (see conv_kernels.hip):
@@ -882,9 +920,52 @@ int run_ups(hfg_handle* h, Launcher& ln, const Layer& L, const float* x, int64_t
   return HFG_OK;
 }
 
+// MRF of stage st (models/hifigan.py:116-131) on X [B][C][L]: out = mean_j ResBlock_j(X)
+// (ResBlock.forward :72-86), or out = ResBlock_only_j(X) alone when only_j >= 0.  R and Tb
+// are B*C*L-float scratch buffers of the layer-per-launch ResBlocks; out must not alias X.
+int run_mrf(hfg_handle* h, Launcher& ln, const Stage& st, const float* X, int64_t B, int64_t L,
+            float* R, float* Tb, float* out, const int32_t* lens, int only_j) {
+  const hfg_config& c = h->cfg;
+  int rc;
+  int idx = 0;
+  for (int j = 0; j < c.n_res; ++j) {
+    if (only_j >= 0 && j != only_j) {
+      idx += c.n_dil[j];
+      continue;
+    }
+    const int mode = only_j >= 0 ? 0 : ((j > 0 ? 1 : 0) | (j == c.n_res - 1 ? 2 : 0));
+    if (st.rbs[j].fused) {
+      rc = run_resblock(h, ln, st.rbs[j], X, B, L, out, mode, (float)c.n_res, lens);
+      if (rc) return rc;
+      idx += c.n_dil[j];
+      continue;
+    }
+    for (int m = 0; m < c.n_dil[j]; ++m, ++idx) {
+      const float* src = (m == 0) ? X : R;
+      const Layer& L1 = h->layers[st.conv1[idx]];
+      const Layer& L2 = h->layers[st.conv2[idx]];
+      // xt = lrelu(conv1(lrelu(x)))
+      rc = run_conv(h, ln, L1, src, B, L, Tb, true, true, nullptr, nullptr, 0, 1.f, lens);
+      if (rc) return rc;
+      const bool last = (m == c.n_dil[j] - 1);
+      if (!last) {
+        // x = x + conv2(xt)
+        rc = run_conv(h, ln, L2, Tb, B, L, R, false, false, src, nullptr, 0, 1.f, lens);
+      } else {
+        rc = run_conv(h, ln, L2, Tb, B, L, nullptr, false, false, src, out, mode,
+                      (float)c.n_res, lens);
+      }
+      if (rc) return rc;
+    }
+  }
+  return HFG_OK;
+}
+
+// taps (inspection, hfg_forward_taps): taps[0] <- conv_pre output, taps[1 + 2i] <- ups[i]
+// output, taps[2 + 2i] <- mrfs[i] output (models/hifigan.py:238-251); NULL entries skipped.
 int forward_impl(hfg_handle* h, const float* mel, int64_t B, int64_t T, const hfg_forward_opts* o,
                  float* wav, int64_t out_len, void* ws, size_t ws_len, hipStream_t stream,
-                 int part = 0) {
+                 int part = 0, float* const* taps = nullptr) {
   if (!mel || !wav) return fail(HFG_EINVAL, "mel / wav pointer is NULL");
   const bool btc = o && o->mel_layout == HFG_MEL_BTC;
   if (o && o->mel_layout != HFG_MEL_BCT && o->mel_layout != HFG_MEL_BTC)
@@ -929,10 +1010,17 @@ int forward_impl(hfg_handle* h, const float* mel, int64_t B, int64_t T, const hf
     lt = table;
   }
   auto lens_at = [&](int s) { return lt ? lt + (size_t)s * B : nullptr; };
+  auto tap = [&](int k, const float* src, int64_t n) -> int {
+    if (!taps || !taps[k]) return HFG_OK;
+    hipError_t e = hipMemcpyAsync(taps[k], src, sizeof(float) * (size_t)n,
+                                  hipMemcpyDeviceToDevice, stream);
+    return e == hipSuccess ? HFG_OK : hip_fail(e, "hipMemcpyAsync(tap)");
+  };
   // conv_pre  (models/hifigan.py:238)
   rc = run_conv(h, ln, h->layers[h->conv_pre], mel, B, T, R, false, false, nullptr, nullptr, 0,
                 1.f, lens_at(0), btc);
   if (rc) return rc;
+  if ((rc = tap(0, R, B * c.c0 * T))) return rc;
   const float* cur = R;
   for (int i = 0; i < c.n_up; ++i) {
     const Stage& st = h->stages[i];
@@ -940,36 +1028,11 @@ int forward_impl(hfg_handle* h, const float* mel, int64_t B, int64_t T, const hf
     // lrelu -> ups[i]  (models/hifigan.py:244-245)
     rc = run_ups(h, ln, h->layers[st.conv_ups], cur, B, Lin, L, X, lens_at(i), lens_at(i + 1));
     if (rc) return rc;
+    if ((rc = tap(1 + 2 * i, X, B * st.C * L))) return rc;
     // MRF (models/hifigan.py:116-131) of ResBlocks (:72-86)
-    int idx = 0;
-    for (int j = 0; j < c.n_res; ++j) {
-      const int mode = (j > 0 ? 1 : 0) | (j == c.n_res - 1 ? 2 : 0);
-      if (st.rbs[j].fused) {
-        rc = run_resblock(h, ln, st.rbs[j], X, B, L, MRF, mode, (float)c.n_res, lens_at(i + 1));
-        if (rc) return rc;
-        idx += c.n_dil[j];
-        continue;
-      }
-      for (int m = 0; m < c.n_dil[j]; ++m, ++idx) {
-        const float* src = (m == 0) ? X : R;
-        const Layer& L1 = h->layers[st.conv1[idx]];
-        const Layer& L2 = h->layers[st.conv2[idx]];
-        // xt = lrelu(conv1(lrelu(x)))
-        rc = run_conv(h, ln, L1, src, B, L, Tb, true, true, nullptr, nullptr, 0, 1.f,
-                      lens_at(i + 1));
-        if (rc) return rc;
-        const bool last = (m == c.n_dil[j] - 1);
-        if (!last) {
-          // x = x + conv2(xt)
-          rc = run_conv(h, ln, L2, Tb, B, L, R, false, false, src, nullptr, 0, 1.f,
-                        lens_at(i + 1));
-        } else {
-          rc = run_conv(h, ln, L2, Tb, B, L, nullptr, false, false, src, MRF, mode,
-                        (float)c.n_res, lens_at(i + 1));
-        }
-        if (rc) return rc;
-      }
-    }
+    rc = run_mrf(h, ln, st, X, B, L, R, Tb, MRF, lens_at(i + 1), -1);
+    if (rc) return rc;
+    if ((rc = tap(2 + 2 * i, MRF, B * st.C * L))) return rc;
     cur = MRF;
   }
   // lrelu -> conv_post -> tanh  (models/hifigan.py:254-256)
@@ -1025,18 +1088,7 @@ int forward_split(hfg_handle* h, const float* mel, int64_t B, int64_t T,
   return rc;
 }
 
-}  // namespace
-
-// ============================================================================
-// C ABI
-// ============================================================================
-extern "C" {
-
-const char* hfg_version(void) { return "hifigan_hip 0.2.0 gfx950 fp32-mfma bf16x3-mfma"; }
-
-const char* hfg_last_error(void) { return g_err.c_str(); }
-
-int hfg_create(const hfg_config* cfg, int device, hfg_handle** out) {
+int create_impl(const hfg_config* cfg, bool mrf_only, int device, hfg_handle** out) {
   if (!out) return fail(HFG_EINVAL, "out is NULL");
   *out = nullptr;
   int rc = validate_config(cfg);
@@ -1050,6 +1102,7 @@ int hfg_create(const hfg_config* cfg, int device, hfg_handle** out) {
   hfg_handle* h = new (std::nothrow) hfg_handle();
   if (!h) return fail(HFG_ENOMEM, "out of host memory");
   h->cfg = *cfg;
+  h->mrf_only = mrf_only;
   h->device = device;
   if (const char* dbg = getenv("HFG_DEBUG_FLAGS")) h->dbg_flags = atoi(dbg);
   if (const char* bt = getenv("HFG_BF16X3_BIGTILE")) {
@@ -1065,9 +1118,50 @@ int hfg_create(const hfg_config* cfg, int device, hfg_handle** out) {
     const int v = atoi(we);
     if (v == 4 || v == 8) h->rb_waves_n32 = v;
   }
-  build_layers(h);
+  rc = build_layers(h);
+  if (rc) {
+    delete h;
+    return rc;
+  }
   *out = h;
   return HFG_OK;
+}
+
+}  // namespace
+
+// ============================================================================
+// C ABI
+// ============================================================================
+extern "C" {
+
+const char* hfg_version(void) { return "hifigan_hip 0.2.0 gfx950 fp32-mfma bf16x3-mfma"; }
+
+const char* hfg_last_error(void) { return g_err.c_str(); }
+
+int hfg_create(const hfg_config* cfg, int device, hfg_handle** out) {
+  return create_impl(cfg, false, device, out);
+}
+
+int hfg_mrf_create(const hfg_mrf_config* mc, int device, hfg_handle** out) {
+  if (!out) return fail(HFG_EINVAL, "out is NULL");
+  *out = nullptr;
+  if (!mc) return fail(HFG_EINVAL, "config is NULL");
+  if (mc->channels <= 0) return fail(HFG_EINVAL, "channels must be > 0");
+  // the generator-level config of one MRF stage: validate_config checks the ResBlock lists
+  hfg_config c{};
+  c.n_mels = 1;
+  c.n_up = 1;
+  c.up_rates[0] = 1;
+  c.up_kernels[0] = 1;
+  c.c0 = 2 * mc->channels;
+  c.n_res = mc->n_res;
+  for (int j = 0; j < HFG_MAX_RES; ++j) {
+    c.res_kernels[j] = mc->res_kernels[j];
+    c.n_dil[j] = mc->n_dil[j];
+    for (int m = 0; m < HFG_MAX_DIL; ++m) c.dil[j][m] = mc->dil[j][m];
+  }
+  c.dtype = mc->dtype;
+  return create_impl(&c, true, device, out);
 }
 
 void hfg_destroy(hfg_handle* h) {
@@ -1093,6 +1187,7 @@ int hfg_set_weight(hfg_handle* h, const char* name, const void* data, const int6
                    int ndim, int is_device) {
   if (!h || !name || !data || (!shape && ndim > 0))
     return fail(HFG_EINVAL, "NULL argument to hfg_set_weight");
+  std::lock_guard<std::recursive_mutex> lk(h->mu);
   std::string key(name);
   std::vector<int64_t> shp(shape, shape + ndim);
   size_t n = 1;
@@ -1164,21 +1259,24 @@ int hfg_set_weight(hfg_handle* h, const char* name, const void* data, const int6
 
 int hfg_commit_weights(hfg_handle* h) {
   if (!h) return fail(HFG_EINVAL, "handle is NULL");
+  std::lock_guard<std::recursive_mutex> lk(h->mu);
   return do_commit(h);
 }
 
 int64_t hfg_out_len(const hfg_handle* h, int64_t T) {
-  if (!h || T <= 0) return -1;
+  if (!h || T <= 0 || h->mrf_only) return -1;
   return shapes_for(h, 1, T).L.back();
 }
 
 size_t hfg_workspace_bytes(const hfg_handle* h, int64_t B, int64_t T) {
-  if (!h || B <= 0 || T <= 0) return 0;
+  if (!h || B <= 0 || T <= 0 || h->mrf_only) return 0;
   return ws_bytes_for(h, B, T);
 }
 
 int hfg_reserve(hfg_handle* h, int64_t B, int64_t T) {
   if (!h) return fail(HFG_EINVAL, "handle is NULL");
+  if (h->mrf_only) return fail(HFG_EINVAL, "MRF-only handle has no generator workspace");
+  std::lock_guard<std::recursive_mutex> lk(h->mu);
   if (h->device < 0) return fail(HFG_EINVAL, "host-only handle");
   if (B <= 0 || T <= 0) return fail(HFG_EINVAL, "B and T must be > 0");
   const size_t need = ws_bytes_for(h, B, T);
@@ -1203,6 +1301,8 @@ int hfg_forward_ex(hfg_handle* h, const float* mel, int64_t B, int64_t T,
                    size_t workspace_bytes, void* stream) {
   if (!h) return fail(HFG_EINVAL, "handle is NULL");
   if (h->device < 0) return fail(HFG_EINVAL, "host-only handle cannot run forward");
+  if (h->mrf_only) return fail(HFG_EINVAL, "MRF-only handle: use hfg_mrf_forward");
+  std::lock_guard<std::recursive_mutex> lk(h->mu);
   if (!workspace) return fail(HFG_EINVAL, "workspace is NULL");
   DeviceGuard g(h->device);
   if (!g.ok) return fail(HFG_ENODEV, "hipSetDevice(%d) failed", h->device);
@@ -1218,6 +1318,8 @@ int hfg_forward_ws(hfg_handle* h, const float* mel, int64_t B, int64_t T, float*
                    int64_t out_len, void* workspace, size_t workspace_bytes, void* stream) {
   if (!h) return fail(HFG_EINVAL, "handle is NULL");
   if (h->device < 0) return fail(HFG_EINVAL, "host-only handle cannot run forward");
+  if (h->mrf_only) return fail(HFG_EINVAL, "MRF-only handle: use hfg_mrf_forward");
+  std::lock_guard<std::recursive_mutex> lk(h->mu);
   if (!workspace) return fail(HFG_EINVAL, "workspace is NULL");
   DeviceGuard g(h->device);
   if (!g.ok) return fail(HFG_ENODEV, "hipSetDevice(%d) failed", h->device);
@@ -1233,13 +1335,90 @@ int hfg_forward(hfg_handle* h, const float* mel, int64_t B, int64_t T, float* wa
                 int64_t out_len, void* stream) {
   if (!h) return fail(HFG_EINVAL, "handle is NULL");
   if (h->device < 0) return fail(HFG_EINVAL, "host-only handle cannot run forward");
+  if (h->mrf_only) return fail(HFG_EINVAL, "MRF-only handle: use hfg_mrf_forward");
+  std::lock_guard<std::recursive_mutex> lk(h->mu);
   int rc = hfg_reserve(h, B, T);
   if (rc) return rc;
   return hfg_forward_ws(h, mel, B, T, wav, out_len, h->ws, h->ws_bytes, stream);
 }
 
+// ---- one MRF / one ResBlock (MRF-only handles, hfg_mrf_create) ---------------
+namespace {
+int mrf_check(hfg_handle* h, const float* x, int64_t B, int64_t L, float* y, void* ws) {
+  if (!h) return fail(HFG_EINVAL, "handle is NULL");
+  if (!h->mrf_only) return fail(HFG_EINVAL, "not an MRF handle (hfg_mrf_create)");
+  if (h->device < 0) return fail(HFG_EINVAL, "host-only handle cannot run forward");
+  if (!x || !y || !ws) return fail(HFG_EINVAL, "x / y / workspace pointer is NULL");
+  if (x == y) return fail(HFG_EINVAL, "y must not alias x");
+  if (B <= 0 || L <= 0) return fail(HFG_EINVAL, "B and L must be > 0");
+  if ((int64_t)h->stages[0].C * L > ((int64_t)1 << 30))
+    return fail(HFG_EINVAL, "per-item activation exceeds 2^30 elements");
+  return HFG_OK;
+}
+size_t mrf_ws_bytes(const hfg_handle* h, int64_t B, int64_t L) {
+  const size_t one = ((sizeof(float) * (size_t)B * h->stages[0].C * (size_t)L) + 255) & ~(size_t)255;
+  return 2 * one;
+}
+int mrf_run(hfg_handle* h, int only_j, const float* x, int64_t B, int64_t L, float* y, void* ws,
+            size_t ws_bytes, void* stream) {
+  int rc = mrf_check(h, x, B, L, y, ws);
+  if (rc) return rc;
+  std::lock_guard<std::recursive_mutex> lk(h->mu);
+  if (ws_bytes < mrf_ws_bytes(h, B, L)) return fail(HFG_EINVAL, "workspace too small");
+  DeviceGuard g(h->device);
+  if (!g.ok) return fail(HFG_ENODEV, "hipSetDevice(%d) failed", h->device);
+  if (h->dirty && (rc = do_commit(h))) return rc;
+  ++h->fwd_count;
+  float* R = static_cast<float*>(ws);
+  float* Tb = R + mrf_ws_bytes(h, B, L) / 2 / sizeof(float);
+  Launcher ln{h, reinterpret_cast<hipStream_t>(stream), 0};
+  return run_mrf(h, ln, h->stages[0], x, B, L, R, Tb, y, nullptr, only_j);
+}
+}  // namespace
+
+size_t hfg_mrf_workspace_bytes(const hfg_handle* h, int64_t B, int64_t L) {
+  if (!h || !h->mrf_only || B <= 0 || L <= 0) return 0;
+  return mrf_ws_bytes(h, B, L);
+}
+
+int hfg_mrf_forward(hfg_handle* h, const float* x, int64_t B, int64_t L, float* y,
+                    void* workspace, size_t workspace_bytes, void* stream) {
+  return mrf_run(h, -1, x, B, L, y, workspace, workspace_bytes, stream);
+}
+
+int hfg_resblock_forward(hfg_handle* h, int j, const float* x, int64_t B, int64_t L, float* y,
+                         void* workspace, size_t workspace_bytes, void* stream) {
+  if (h && (j < 0 || j >= h->cfg.n_res)) return fail(HFG_EINVAL, "resblock index %d out of range", j);
+  return mrf_run(h, j, x, B, L, y, workspace, workspace_bytes, stream);
+}
+
+// ---- content hash of parameter tensors -----------------------------------------
+int hfg_checksum32(const void* const* ptrs, const int64_t* nbytes, int n, uint32_t* out,
+                   void* stream) {
+  if (n < 0 || (n > 0 && (!ptrs || !nbytes || !out))) return fail(HFG_EINVAL, "bad arguments");
+  if (n == 0) return HFG_OK;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  hipError_t e = hipMemsetAsync(out, 0, sizeof(uint32_t) * (size_t)n, st);
+  if (e != hipSuccess) return hip_fail(e, "hipMemsetAsync(checksum)");
+  for (int base = 0; base < n; base += hfg::kChecksumMax) {
+    hfg::ChecksumArgs a{};
+    a.base = base;
+    a.count = std::min(hfg::kChecksumMax, n - base);
+    for (int i = 0; i < a.count; ++i) {
+      if (nbytes[base + i] % 4 != 0 || (nbytes[base + i] > 0 && !ptrs[base + i]))
+        return fail(HFG_EINVAL, "tensor %d: size must be a multiple of 4 bytes", base + i);
+      a.p[i] = static_cast<const uint32_t*>(ptrs[base + i]);
+      a.n[i] = nbytes[base + i] / 4;
+    }
+    e = hfg::launch_checksum(a, out, st);
+    if (e != hipSuccess) return hip_fail(e, "launch checksum");
+  }
+  return HFG_OK;
+}
+
 int hfg_set_streams(hfg_handle* h, int n) {
   if (!h) return fail(HFG_EINVAL, "handle is NULL");
+  std::lock_guard<std::recursive_mutex> lk(h->mu);
   if (n != 1 && n != 2) return fail(HFG_EINVAL, "streams must be 1 or 2 (got %d)", n);
   h->split = n;
   return HFG_OK;
@@ -1247,12 +1426,14 @@ int hfg_set_streams(hfg_handle* h, int n) {
 
 int hfg_set_profiling(hfg_handle* h, int enable) {
   if (!h) return fail(HFG_EINVAL, "handle is NULL");
+  std::lock_guard<std::recursive_mutex> lk(h->mu);
   h->profiling = enable != 0;
   return HFG_OK;
 }
 
 int hfg_profile_reset(hfg_handle* h) {
   if (!h) return fail(HFG_EINVAL, "handle is NULL");
+  std::lock_guard<std::recursive_mutex> lk(h->mu);
   DeviceGuard g(h->device);
   for (auto& r : h->prof)
     if (r.e1) (void)hipEventSynchronize(r.e1);
@@ -1262,6 +1443,7 @@ int hfg_profile_reset(hfg_handle* h) {
 
 int hfg_profile_summary(hfg_handle* h, char* buf, size_t buflen) {
   if (!h || !buf || buflen == 0) return fail(HFG_EINVAL, "bad arguments");
+  std::lock_guard<std::recursive_mutex> lk(h->mu);
   DeviceGuard g(h->device);
   struct Agg {
     int launches = 0;
@@ -1389,6 +1571,26 @@ int hfg_debug_packed_resblock(hfg_handle* h, int stage, int j, float* out, size_
   memcpy(out, h->packed_host.data() + rb.w_off, sizeof(float) * rb.w_len);
   memcpy(out + rb.w_len, h->packed_host.data() + rb.b_off, sizeof(float) * rb.b_len);
   return HFG_OK;
+}
+
+int hfg_forward_taps(hfg_handle* h, const float* mel, int64_t B, int64_t T, float* wav,
+                     int64_t out_len, void* workspace, size_t workspace_bytes,
+                     float* const* taps, int n_taps, void* stream) {
+  if (!h) return fail(HFG_EINVAL, "handle is NULL");
+  if (h->device < 0 || h->mrf_only) return fail(HFG_EINVAL, "not a generator device handle");
+  if (!workspace) return fail(HFG_EINVAL, "workspace is NULL");
+  if (taps && n_taps != 1 + 2 * h->cfg.n_up)
+    return fail(HFG_EINVAL, "n_taps must be 1 + 2 * n_up = %d", 1 + 2 * h->cfg.n_up);
+  std::lock_guard<std::recursive_mutex> lk(h->mu);
+  DeviceGuard g(h->device);
+  if (!g.ok) return fail(HFG_ENODEV, "hipSetDevice(%d) failed", h->device);
+  if (h->dirty) {
+    int rc = do_commit(h);
+    if (rc) return rc;
+  }
+  ++h->fwd_count;
+  return forward_impl(h, mel, B, T, nullptr, wav, out_len, workspace, workspace_bytes,
+                      reinterpret_cast<hipStream_t>(stream), 0, taps);
 }
 
 }  // extern "C"

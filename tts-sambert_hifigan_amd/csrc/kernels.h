@@ -59,6 +59,9 @@ constexpr TileCfg kTiles[TILE_COUNT] = {
     {1, 4, 1, 4},  // M32 :  32 x 512 tile, 4 waves of 32x128
 };
 
+// the fp32 kernel of `tile` handles kt taps at dilation dil (staging registers, LDS)
+bool fp32_conv_supported(int tile, int kt, int dil);
+
 inline TileId tile_for_rows(int M) {
   if (M >= 128) return TILE_M128;
   if (M >= 64) return TILE_M64;
@@ -108,6 +111,10 @@ inline int bf16x3_tile_for_rows(int M, int big_tile = 0) {
   return M >= 128 ? big_tile : (M >= 64 ? 1 : (M >= 32 ? 2 : -1));
 }
 size_t bf16x3_lds_bytes(int tile, int kt, int dil);
+// the bf16x3 layer kernel handles kt taps at dilation dil (else the fp32 kernel runs)
+inline bool bf16x3_supported(int kt, int dil) {
+  return dil >= 1 && dil <= kMaxDil && kt >= 1 && kt <= 16 && (kt - 1) * dil <= kBf16x3MaxHalo;
+}
 hipError_t launch_conv_bf16x3(int tile, int kt, bool ups, const ConvParams& p, int n_tiles,
                               int m_tiles, int batch, hipStream_t stream, const char** name);
 
@@ -180,11 +187,26 @@ hipError_t launch_resblock16_bf16x3(int C, int waves_n, int kt, const RbParams& 
 hipError_t launch_conv(TileId tile, int kt, bool ups, const ConvParams& p, int n_tiles,
                        int m_tiles, int batch, hipStream_t stream, const char** name);
 
+// conv_post + tanh: input rows staged in LDS kConvPostCB channels at a time
+constexpr int kConvPostCB = 32;
+inline size_t conv_post_lds_bytes(int C) {
+  return sizeof(float) * ((size_t)((C * 7 + 3) & ~3) + (size_t)(C < kConvPostCB ? C : kConvPostCB) * (256 + 6));
+}
 // conv_post + tanh: wav[b][t] = tanh(bias + sum_{c,j} w[c][j] * lrelu(x[b][c][t+j-3]))
 // for t < lens[b] (lens null = L); 0 beyond.
 hipError_t launch_conv_post(const float* x, int64_t x_bs, int C, int L, const float* w,
                             const float* bias, float* wav, const int32_t* lens, int batch,
                             hipStream_t stream, const char** name);
+
+// Content hash of up to kChecksumMax fp32 tensors per launch: out[base + i] +=
+// sum_w mix(word_w, w) over tensor i's n[i] 32-bit words (out zeroed by the caller).
+constexpr int kChecksumMax = 64;
+struct ChecksumArgs {
+  const uint32_t* p[kChecksumMax];
+  int64_t n[kChecksumMax];
+  int count, base;
+};
+hipError_t launch_checksum(const ChecksumArgs& a, uint32_t* out, hipStream_t stream);
 
 // Per-stage valid lengths of a ragged batch: out[s*B + b] = length after s
 // upsample stages of an utterance with lens[b] frames (clamped to [0, T]).

@@ -38,13 +38,123 @@ def get_padding(kernel_size: int, dilation: int = 1) -> int:
     return int((kernel_size * dilation - dilation) / 2)
 
 
-class ResBlock(nn.Module):
-    """Parameter container with the reference layout (models/hifigan.py:34-70):
-    ``convs1[m]`` = Conv1d(C, C, k, dilation=d_m), ``convs2[m]`` = Conv1d(C, C, k).
-    Its computation runs inside the fused Generator schedule on the GPU."""
+class _HipWeights(nn.Module):
+    """Weight tracking shared by the modules that run on a C-ABI handle.
 
-    def __init__(self, channels: int, kernel_size: int = 3, dilation: Tuple[int, ...] = (1, 3, 5)):
+    The parameters stay in ordinary ``nn.Conv1d`` / ``nn.ConvTranspose1d``
+    containers; a handle per device holds them packed in the kernels' layout.  They
+    are re-packed before a forward when any parameter was replaced, resized or
+    moved (data_ptr / shape), bumped its autograd version (in-place ops, ``copy_``
+    under no_grad), after ``load_state_dict`` / ``.to()`` / ``refresh_weights()``,
+    and — with ``verify_weights`` (default) — when a device-side content hash of
+    the parameters (``hfg_checksum32``) differs from the one at the last commit,
+    which catches edits through ``param.data`` that leave the version counter
+    untouched.  The hash costs one small D2H read (a stream sync) per forward; it
+    is skipped while a hipGraph is being captured.  Set ``verify_weights = False``
+    for fully asynchronous launches and call ``refresh_weights()`` after editing
+    weights through ``.data``.
+    """
+
+    verify_weights = True
+
+    def _hip_setup(self, precision: str):
+        self._hfg_handles: Dict[int, _lib.Handle] = {}
+        self._hfg_fingerprint: Dict[int, tuple] = {}
+        self._hfg_checksum: Dict[int, torch.Tensor] = {}
+        self.precision = precision
+        self.register_load_state_dict_post_hook(lambda m, _incompatible: m.refresh_weights())
+
+    def refresh_weights(self):
+        """Force a re-pack of the parameters before the next forward."""
+        self._hfg_fingerprint = {}
+        self._hfg_checksum = {}
+        return self
+
+    def _apply(self, fn, *args, **kwargs):
+        out = super()._apply(fn, *args, **kwargs)
+        self.refresh_weights()
+        return out
+
+    # subclasses: (key, tensor) of every parameter in the handle's key space, and the handle
+    def _hip_weight_items(self):
+        raise NotImplementedError
+
+    def _hip_new_handle(self, idx: int) -> _lib.Handle:
+        raise NotImplementedError
+
+    def _handle_for(self, device: torch.device) -> _lib.Handle:
+        idx = device.index if device.index is not None else torch.cuda.current_device()
+        h = self._hfg_handles.get(idx)
+        if h is None:
+            h = self._hip_new_handle(idx)
+            self._hfg_handles[idx] = h
+        items = list(self._hip_weight_items())
+        fp = tuple((k, t.data_ptr(), t._version, tuple(t.shape), str(t.device)) for k, t in items)
+        stale = self._hfg_fingerprint.get(idx) != fp
+        dev_ts = [t.detach() for _, t in items if t.is_cuda and t.dtype == torch.float32
+                  and t.is_contiguous()]
+        check = (self.verify_weights and dev_ts and
+                 not torch.cuda.is_current_stream_capturing())
+        cks = None
+        if not stale and check:
+            cks = _lib.checksum32(dev_ts)
+            stale = not torch.equal(cks, self._hfg_checksum.get(idx, torch.empty(0)))
+        if stale:
+            for k, t in items:
+                h.set_weight(k, t)
+            h.commit()
+            self._hfg_fingerprint[idx] = fp
+            if check:
+                self._hfg_checksum[idx] = cks if cks is not None else _lib.checksum32(dev_ts)
+        return h
+
+    @staticmethod
+    def _conv_items(module: nn.Module, prefix: str = ""):
+        for name, mod in module.named_modules():
+            if not isinstance(mod, (nn.Conv1d, nn.ConvTranspose1d)):
+                continue
+            if hasattr(mod, "weight_g") and hasattr(mod, "weight_v"):
+                yield prefix + name + ".weight_g", mod.weight_g
+                yield prefix + name + ".weight_v", mod.weight_v
+            else:
+                yield prefix + name + ".weight", mod.weight
+            yield prefix + name + ".bias", mod.bias
+
+    def _run_block(self, x: torch.Tensor, channels: int, resblock: int) -> torch.Tensor:
+        """y = MRF(x) (resblock < 0) or ResBlock_resblock(x) on the HIP device."""
+        if not isinstance(x, torch.Tensor) or x.dim() != 3 or x.shape[1] != channels:
+            raise RuntimeError(f"expected x [B, {channels}, T], got {getattr(x, 'shape', type(x))}")
+        if not x.is_cuda:
+            raise RuntimeError("the MI355X ResBlock / MRF run on the HIP device only; move x to "
+                               "'cuda' (there is no CPU fallback)")
+        if torch.is_grad_enabled() and x.requires_grad:
+            raise NotImplementedError("inference-only HIP path: no autograd")
+        B, _, L = x.shape
+        if B == 0 or L == 0:
+            raise RuntimeError("empty input")
+        xc = x.detach().to(torch.float32).contiguous()
+        with torch.cuda.device(x.device):
+            h = self._handle_for(x.device)
+            y = torch.empty_like(xc)
+            ws_bytes = h.mrf_workspace_bytes(B, L)
+            ws = torch.empty(ws_bytes, dtype=torch.uint8, device=x.device)
+            h.mrf_forward(xc.data_ptr(), B, L, y.data_ptr(), ws.data_ptr(), ws_bytes,
+                          torch.cuda.current_stream(x.device).cuda_stream, resblock=resblock)
+        return y
+
+
+class ResBlock(_HipWeights):
+    """ResBlock (models/hifigan.py:26-86): ``convs1[m]`` = Conv1d(C, C, k, dilation=d_m),
+    ``convs2[m]`` = Conv1d(C, C, k); forward = for each m: x += conv2(lrelu(conv1(lrelu(x)))).
+    Inside a Generator its computation is part of the fused schedule; called on its own
+    it runs ``hfg_resblock_forward`` on an MRF handle of this one block."""
+
+    def __init__(self, channels: int, kernel_size: int = 3, dilation: Tuple[int, ...] = (1, 3, 5),
+                 *, precision: str = "fp32"):
         super().__init__()
+        self.channels = channels
+        self.kernel_size = kernel_size
+        self.dilation = tuple(dilation)
         self.convs1 = nn.ModuleList()
         self.convs2 = nn.ModuleList()
         for d in dilation:
@@ -52,27 +162,55 @@ class ResBlock(nn.Module):
                                          padding=get_padding(kernel_size, d)))
             self.convs2.append(nn.Conv1d(channels, channels, kernel_size, stride=1, dilation=1,
                                          padding=get_padding(kernel_size, 1)))
+        self._hip_setup(precision)
 
-    def forward(self, x):
-        raise NotImplementedError(
-            "ResBlock runs only inside HiFiGANGenerator.forward on the HIP path")
+    def _hip_weight_items(self):
+        return self._conv_items(self, "resblocks.0.")
+
+    def _hip_new_handle(self, idx):
+        cfg = _lib.make_mrf_config(self.channels, [self.kernel_size], [list(self.dilation)],
+                                   precision=self.precision)
+        return _lib.Handle(cfg, idx, mrf=True)
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        """x [B, C, T] -> [B, C, T] (models/hifigan.py:72-86)."""
+        if not self.dilation:
+            return x
+        return self._run_block(x, self.channels, 0)
 
 
-class MRF(nn.Module):
-    """Parameter container with the reference layout (models/hifigan.py:96-114)."""
+class MRF(_HipWeights):
+    """Multi-Receptive Field module (models/hifigan.py:89-131): the mean of its
+    ResBlocks' outputs on the same input.  Called on its own it runs
+    ``hfg_mrf_forward`` on an MRF handle with this module's state_dict keys."""
 
     def __init__(self, channels: int, resblock_kernel_sizes: List[int] = [3, 7, 11],
-                 resblock_dilation_sizes: List[List[int]] = [[1, 3, 5], [1, 3, 5], [1, 3, 5]]):
+                 resblock_dilation_sizes: List[List[int]] = [[1, 3, 5], [1, 3, 5], [1, 3, 5]],
+                 *, precision: str = "fp32"):
         super().__init__()
+        self.channels = channels
+        self.resblock_kernel_sizes = list(resblock_kernel_sizes)
+        self.resblock_dilation_sizes = [list(d) for d in resblock_dilation_sizes]
         self.resblocks = nn.ModuleList()
         for kernel_size, dilations in zip(resblock_kernel_sizes, resblock_dilation_sizes):
-            self.resblocks.append(ResBlock(channels, kernel_size, tuple(dilations)))
+            self.resblocks.append(ResBlock(channels, kernel_size, tuple(dilations),
+                                           precision=precision))
+        self._hip_setup(precision)
 
-    def forward(self, x):
-        raise NotImplementedError("MRF runs only inside HiFiGANGenerator.forward on the HIP path")
+    def _hip_weight_items(self):
+        return self._conv_items(self)
+
+    def _hip_new_handle(self, idx):
+        cfg = _lib.make_mrf_config(self.channels, self.resblock_kernel_sizes,
+                                   self.resblock_dilation_sizes, precision=self.precision)
+        return _lib.Handle(cfg, idx, mrf=True)
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        """x [B, C, T] -> mean_j ResBlock_j(x) [B, C, T] (models/hifigan.py:116-131)."""
+        return self._run_block(x, self.channels, -1)
 
 
-class HiFiGANGenerator(nn.Module):
+class HiFiGANGenerator(_HipWeights):
     """HiFi-GAN Generator, mel [B, n_mels, Tfrm] → wav [B, 1, T_wav] on MI355X.
 
     Same constructor as models/hifigan.py:149-158.
@@ -105,53 +243,38 @@ class HiFiGANGenerator(nn.Module):
             out_channels = upsample_initial_channel // (2 ** (i + 1))
             self.ups.append(nn.ConvTranspose1d(in_channels, out_channels, kernel_size=k, stride=u,
                                                padding=(k - u) // 2))
-            self.mrfs.append(MRF(out_channels, resblock_kernel_sizes, resblock_dilation_sizes))
+            self.mrfs.append(MRF(out_channels, resblock_kernel_sizes, resblock_dilation_sizes,
+                                 precision=precision))
         final_channels = upsample_initial_channel // (2 ** self.num_upsamples)
         self.conv_post = nn.Conv1d(final_channels, 1, kernel_size=7, stride=1, padding=3)
 
         self._hfg_args = (n_mels, upsample_rates, upsample_kernel_sizes, upsample_initial_channel,
                           resblock_kernel_sizes, resblock_dilation_sizes)
-        self._hfg_handles: Dict[int, _lib.Handle] = {}
-        self._hfg_fingerprint: Dict[int, tuple] = {}
+        self._hip_setup(precision)
         self.set_precision(precision)
 
     def set_precision(self, precision: str):
         """"fp32" (exact fp32 MFMA, default) or "bf16x3" (fp32 operands split into
-        two bf16 halves on the bf16 matrix cores; within ~1e-6 of the reference)."""
+        two bf16 halves on the bf16 matrix cores; within ~1e-5 of the reference at
+        default weight scale).  Applies to the MRF / ResBlock submodules too."""
         self._hfg_cfg = _lib.make_config(*self._hfg_args, precision=precision)
-        self.precision = precision
-        self._hfg_handles = {}
-        self._hfg_fingerprint = {}
+        for m in self.modules():
+            if isinstance(m, _HipWeights):
+                m.precision = precision
+                m._hfg_handles = {}
+                m.refresh_weights()
         return self
 
     # ------------------------------------------------------------------
-    def _weight_tensors(self):
+    def _hip_weight_items(self):
         """(state_dict-style key, tensor) of every parameter the kernels need,
         with weight_g / weight_v passed through for weight-normed modules."""
-        for name, mod in self.named_modules():
-            if not isinstance(mod, (nn.Conv1d, nn.ConvTranspose1d)):
-                continue
-            if hasattr(mod, "weight_g") and hasattr(mod, "weight_v"):
-                yield name + ".weight_g", mod.weight_g
-                yield name + ".weight_v", mod.weight_v
-            else:
-                yield name + ".weight", mod.weight
-            yield name + ".bias", mod.bias
+        return self._conv_items(self)
 
-    def _handle_for(self, device: torch.device) -> _lib.Handle:
-        idx = device.index if device.index is not None else torch.cuda.current_device()
-        h = self._hfg_handles.get(idx)
-        if h is None:
-            h = _lib.Handle(self._hfg_cfg, idx)
-            self._hfg_handles[idx] = h
-        tensors = list(self._weight_tensors())
-        fp = tuple((k, t.data_ptr(), t._version, tuple(t.shape)) for k, t in tensors)
-        if self._hfg_fingerprint.get(idx) != fp:
-            for k, t in tensors:
-                h.set_weight(k, t)
-            h.commit()
-            self._hfg_fingerprint[idx] = fp
-        return h
+    _weight_tensors = _hip_weight_items
+
+    def _hip_new_handle(self, idx):
+        return _lib.Handle(self._hfg_cfg, idx)
 
     def hip_handle(self, device=None) -> _lib.Handle:
         """The C-ABI handle for ``device`` with the current weights committed."""
@@ -231,6 +354,33 @@ class HiFiGANGenerator(nn.Module):
                 print(f"[HiFiGANGenerator] After MRF {i}: {torch.Size([B, c, x_len])}")
             print(f"[HiFiGANGenerator] Output wav shape: {wav.shape}")
         return wav
+
+    def forward_with_stages(self, mel: torch.Tensor):
+        """(wav, {stage: tensor}) — the forward (one stream) plus copies of the tensors the
+        reference's forward passes through (models/hifigan.py:238-251): "conv_pre",
+        "ups.i" (after each ConvTranspose1d) and "mrfs.i" (after each MRF).  Inspection
+        entry hfg_forward_taps (include/hifigan_hip_inspect.h); for parity checks."""
+        if not (isinstance(mel, torch.Tensor) and mel.dim() == 3 and mel.is_cuda):
+            raise RuntimeError("expected a HIP mel [B, n_mels, T]")
+        B, _, T = mel.shape
+        mel_c = mel.detach().to(torch.float32).contiguous()
+        with torch.cuda.device(mel.device):
+            h = self._handle_for(mel.device)
+            out_len = h.out_len(T)
+            wav = torch.empty((B, 1, out_len), dtype=torch.float32, device=mel.device)
+            stages = {"conv_pre": torch.empty(B, self.conv_pre.out_channels, T, device=mel.device)}
+            x_len = T
+            for i, up in enumerate(self.ups):
+                u, k = up.stride[0], up.kernel_size[0]
+                x_len = (x_len - 1) * u - 2 * ((k - u) // 2) + k
+                for name in (f"ups.{i}", f"mrfs.{i}"):
+                    stages[name] = torch.empty(B, up.out_channels, x_len, device=mel.device)
+            ws_bytes = h.workspace_bytes(B, T)
+            ws = torch.empty(ws_bytes, dtype=torch.uint8, device=mel.device)
+            h.forward_taps(mel_c.data_ptr(), B, T, wav.data_ptr(), out_len, ws.data_ptr(),
+                           ws_bytes, [t.data_ptr() for t in stages.values()],
+                           torch.cuda.current_stream(mel.device).cuda_stream)
+        return wav, stages
 
     def receptive_field_frames(self) -> int:
         """Upper bound, in mel frames, of how far (each side) an output sample's
