@@ -16,15 +16,28 @@ every kernel launch bracketed by HIP events on that stream (libhifigan_hip profi
 mode); the dominant kernel's achieved TFLOP/s = its algorithmic FLOP ÷ its summed
 launch time (with two streams the halves' intervals overlap, so they cannot be
 attributed to one kernel).
+Also: per-step HIP-event median (median of the timed steps), an
+end-to-end figure with the H2D mel and D2H wav copies on the same stream, and (N=1)
+`traffic` from two live rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE) of this same
+workload, run as child processes before this process touches the GPU.
 cpu_baseline: the oracle's PyTorch-CPU restatement (same ATen ops as the
 reference) on this host's cores, rank 0 / N=1 only, on a bounded sample.
+
+`value` is the whole-job aggregate (all ranks' samples ÷ the max-over-ranks time), as
+the bench contract prescribes; the per-GPU figure the metric name speaks of is
+`value_per_gpu` (identical at N=1).
 """
 from __future__ import annotations
 
 import argparse
+import csv
+import glob
 import json
 import os
+import shutil
+import subprocess
 import sys
+import tempfile
 import time
 
 import numpy as np
@@ -76,7 +89,98 @@ def parse():
                          "a 1-stream profiled pass")
     ap.add_argument("--no-profile", action="store_true",
                     help="do not bracket launches with HIP events (no roofline)")
+    ap.add_argument("--no-pmc", action="store_true",
+                    help="skip the live rocprofv3 FETCH_SIZE / WRITE_SIZE passes (traffic=null)")
+    ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
     return ap.parse_args()
+
+
+# FETCH_SIZE / WRITE_SIZE corrections measured by profiles/pmc_calib.hip on gfx950
+# (known 1 GiB streams; profiles/r02/pmc_calib.json): counter bytes / true bytes.
+PMC_FETCH_SCALE = 0.5   # 4-B and 16-B per lane loads alike
+PMC_WRITE_SCALE = 1.0   # 4-B and 16-B per lane stores alike
+
+
+def _norm(name: str) -> str:
+    name = name.split("(")[0]
+    for pre in ("void ", "hfg::"):
+        if name.startswith(pre):
+            name = name[len(pre):]
+    return name.replace(" ", "")
+
+
+def _host_cores():
+    """(threads to use, description): the CPUs this process may run on, capped by the
+    cgroup CPU quota when one is set (a GPU box shows every host CPU in
+    sched_getaffinity but grants a share of them)."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = max(1, int(int(q) / int(per)))
+    except Exception:
+        quota = None
+    model = ""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except Exception:
+        pass
+    use = min(aff, quota) if quota else aff
+    env = os.environ.get("OMP_NUM_THREADS")
+    desc = (f"{use} threads = sched_getaffinity {aff} CPUs"
+            + (f" capped by the cgroup CPU quota {quota}" if quota else " (no cgroup quota)")
+            + (f"; OMP_NUM_THREADS={env}" if env else "") + (f"; {model}" if model else ""))
+    return use, desc
+
+
+def pmc_traffic(argv_extra):
+    """Per-kernel HBM bytes per launch from two rocprofv3 --pmc passes (FETCH_SIZE and
+    WRITE_SIZE in separate runs, no trace domains: MI355X_MICROARCH.md §HBM) of this
+    workload on one stream.  Runs child processes; call before this process uses the GPU.
+    Returns ({kernel: {fetch, write, bytes}}, note) or (None, reason)."""
+    exe = shutil.which("rocprofv3")
+    if exe is None:
+        return None, "rocprofv3 not found"
+    tmp = tempfile.mkdtemp(prefix="hfg_pmc_", dir="/tmp")
+    env = dict(os.environ, TMPDIR="/tmp")
+    per = {}
+    try:
+        for counter in ("FETCH_SIZE", "WRITE_SIZE"):
+            d = os.path.join(tmp, counter)
+            cmd = ["timeout", "-s", "KILL", "150", exe, "--pmc", counter, "-d", d, "-o", "run",
+                   "--output-format", "csv", "--", sys.executable, os.path.abspath(__file__),
+                   "--pmc-child", "--steps", "2", "--warmup", "1", "--streams", "1",
+                   "--no-profile", "--no-extra", "--no-cpu-baseline", "--no-pmc"] + argv_extra + ["--also"]
+            r = subprocess.run(cmd, cwd="/tmp", env=env, stdout=subprocess.DEVNULL,
+                               stderr=subprocess.PIPE, text=True)
+            if r.returncode != 0:
+                return None, f"rocprofv3 --pmc {counter} pass failed (rc {r.returncode}): " \
+                             f"{r.stderr.strip().splitlines()[-1:] }"
+            files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
+            vals = {}
+            for fpath in files:
+                with open(fpath) as f:
+                    for row in csv.DictReader(f):
+                        if row.get("Counter_Name") == counter:
+                            vals.setdefault(_norm(row["Kernel_Name"]), []).append(
+                                float(row["Counter_Value"]) * 1024.0)
+            if not vals:
+                return None, f"no {counter} rows in the rocprofv3 output"
+            scale = PMC_FETCH_SCALE if counter == "FETCH_SIZE" else PMC_WRITE_SCALE
+            for k, v in vals.items():
+                per.setdefault(k, {})["fetch" if counter == "FETCH_SIZE" else "write"] = \
+                    sum(v) / len(v) / scale
+        for v in per.values():
+            v["bytes"] = v.get("fetch", 0.0) + v.get("write", 0.0)
+        return per, ("live rocprofv3 --pmc FETCH_SIZE and WRITE_SIZE passes of this workload "
+                     f"(1 stream, 3 forwards); FETCH_SIZE / {PMC_FETCH_SCALE}, WRITE_SIZE / "
+                     f"{PMC_WRITE_SCALE} (profiles/pmc_calib.hip calibration), KiB x 1024")
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
 
 
 def cpu_baseline(cfg, sd, frames, budget_s):
@@ -84,7 +188,9 @@ def cpu_baseline(cfg, sd, frames, budget_s):
     [1, 80, frames] utterance after a warm-up, within ~budget_s seconds."""
     from oracle import config as OC, hifigan_torch, prng  # the CPU baseline leg only
     cfg = OC.GenConfig(**cfg.kwargs())
-    threads = torch.get_num_threads()
+    threads, cores_desc = _host_cores()
+    prev = torch.get_num_threads()
+    torch.set_num_threads(threads)
     tsd = hifigan_torch.to_torch_state(sd)
     mel = torch.from_numpy(prng.mel_input(1234, (1, cfg.n_mels, frames)))
     hifigan_torch.generator_forward(tsd, cfg, mel[:, :, :32])  # warm-up
@@ -95,12 +201,13 @@ def cpu_baseline(cfg, sd, frames, budget_s):
         dt = time.perf_counter() - t0
         best = dt if best is None else min(best, dt)
         runs += 1
+    torch.set_num_threads(prev)
     samples = wav.shape[-1]
     return {"value": samples / best, "unit": "audio samples/s", "cores": threads,
             "kind": "port",
             "sample": f"1 utterance [1,{cfg.n_mels},{frames}] of the bench workload, best of {runs} "
-                      f"after warm-up, oracle/hifigan_torch.py (same ATen ops as the reference), "
-                      f"{threads} threads, {os.cpu_count()} host CPUs visible",
+                      f"after warm-up, oracle/hifigan_torch.py (same ATen ops as the reference)",
+            "cores_note": cores_desc,
             "rtf": best / (samples / SAMPLE_RATE)}
 
 
@@ -179,6 +286,11 @@ def main():
     if "RANK" in os.environ and int(os.environ.get("WORLD_SIZE", "1")) > 1:
         rank, world, local_rank = (int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"]),
                                    int(os.environ.get("LOCAL_RANK", "0")))
+    pmc, pmc_note = None, "not collected (--no-pmc or N > 1)"
+    if world == 1 and not args.no_pmc and not args.pmc_child:
+        # before this process initialises the GPU: the passes are child processes
+        pmc, pmc_note = pmc_traffic(["--preset", args.preset, "--batch", str(args.batch),
+                                     "--frames", str(args.frames), "--precision", args.precision])
     if world != args.gpus and rank == 0:
         print(f"[bench] note: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
     assert torch.cuda.is_available(), "bench.py needs MI355X GPUs"
@@ -243,14 +355,20 @@ def main():
         if profile and args.streams == 1:
             h.profile_reset()
             h.set_profiling(True)
+        evs = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize(dev)
         t0 = time.perf_counter()
-        for _ in range(args.steps):
+        evs[0].record(stream)
+        for i in range(args.steps):
             step()
+            evs[i + 1].record(stream)   # the forward joins its aux stream back into `stream`
         torch.cuda.synchronize(dev)
         elapsed = time.perf_counter() - t0
+        step_ms = sorted(evs[i].elapsed_time(evs[i + 1]) for i in range(args.steps))
+        ev_median[precision] = step_ms[len(step_ms) // 2] if len(step_ms) % 2 else \
+            0.5 * (step_ms[len(step_ms) // 2 - 1] + step_ms[len(step_ms) // 2])
         if world > 1:
             dist.barrier()
             t = torch.tensor([elapsed], dtype=torch.float64, device=coll_dev)
@@ -279,10 +397,37 @@ def main():
                 h.set_profiling(False)
                 prof = h.profile_summary()
                 h.set_streams(args.streams)
+        if precision == args.precision and not args.pmc_child:
+            e2e[precision] = end_to_end(step, wav)
         del ws, wav
         return elapsed, prof, out_len
 
+    def end_to_end(step, wav_d):
+        """K steps of: H2D of the mel from pinned host memory, the forward, D2H of the wav
+        into pinned host memory, all on the launch stream (SURVEY.md §8(d) end-to-end)."""
+        mel_h = mel.cpu().pin_memory()
+        wav_h = torch.empty(wav_d.shape, dtype=torch.float32).pin_memory()
+        mel_d = mel
+
+        def one():
+            mel_d.copy_(mel_h, non_blocking=True)
+            step()
+            wav_h.copy_(wav_d, non_blocking=True)
+
+        one()
+        torch.cuda.synchronize(dev)
+        t1 = time.perf_counter()
+        for _ in range(args.steps):
+            one()
+        torch.cuda.synchronize(dev)
+        dt = (time.perf_counter() - t1) / args.steps
+        return {"ms_per_step": dt * 1e3, "samples_per_s": wav_d.numel() / dt,
+                "note": "H2D mel (pinned) + forward + D2H wav (pinned) on one stream, K steps; "
+                        "the copies are not overlapped with the next step's compute"}
+
     prof_ms = {}  # ms/step of the 1-stream roofline pass, per precision
+    ev_median = {}  # per-step HIP-event median (ms) of the value pass, per precision
+    e2e = {}
     elapsed, prof, out_len = measure(args.precision)
     alt = {}
     for prec in args.also:
@@ -325,9 +470,16 @@ def main():
             "global_batch": global_batch,
             "parallelism": f"dp{world} (utterance-sharded, RCCL weight broadcast at init)",
         },
-        "per_gpu": value / world,
+        "value_per_gpu": value / world,
+        "value_note": "value = whole-job aggregate (all ranks' samples / max-over-ranks time, the "
+                      "bench contract); value_per_gpu = value / n_gpus",
         "rtf": (elapsed / args.steps) / (args.batch * out_len / SAMPLE_RATE),
+        "step_ms_hipevent_median": ev_median.get(args.precision),
+        "samples_per_s_hipevent_median": (args.batch * out_len / (ev_median[args.precision] * 1e-3)
+                                          if ev_median.get(args.precision) else None),
     }
+    if args.precision in e2e:
+        line["end_to_end"] = e2e[args.precision]
     def roofline(prof, ms_per_step):
         dom_name, dom = max(prof.items(), key=lambda kv: kv[1]["ms"])
         achieved = dom["flop"] / (dom["ms"] * 1e-3) / 1e12
@@ -357,14 +509,8 @@ def main():
         dom_name, dom = max(prof.items(), key=lambda kv: kv[1]["ms"])
         achieved = dom["flop"] / (dom["ms"] * 1e-3) / 1e12
         traffic = None
-        pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-        if os.path.exists(pmc_path):
-            try:
-                pmc = json.load(open(pmc_path))
-                if dom_name in pmc and pmc[dom_name].get("bytes_per_launch"):
-                    traffic = pmc[dom_name]["bytes_per_launch"]
-            except Exception:
-                traffic = None
+        if pmc and _norm(dom_name) in pmc:
+            traffic = pmc[_norm(dom_name)]["bytes"]
         peak, peak_note = kernel_peak(dom_name)
         line["roofline"] = {
             "bound": "mfma",
@@ -375,6 +521,9 @@ def main():
             "unit": "TFLOP/s",
             "frac": achieved / peak,
             "traffic": traffic,
+            "traffic_note": pmc_note,
+            "traffic_over_alg_bytes": (traffic / (dom["bytes"] / dom["launches"])
+                                       if traffic else None),
             "launches_per_step": dom["launches"] / args.steps,
             "avg_launch_ms": dom["ms"] / dom["launches"],
             "flop_per_launch": dom["flop"] / dom["launches"],
@@ -390,9 +539,14 @@ def main():
         all_flop = sum(v["flop"] for v in prof.values()) / args.steps
         all_bytes = sum(v["bytes"] for v in prof.values()) / args.steps
         step_s = elapsed / args.steps
+        issue = 3.0 if args.precision == "bf16x3" else 1.0
         line["roofline_step"] = {
             "compute_TFLOPs": all_flop / step_s / 1e12,
-            "compute_frac_fp32": all_flop / step_s / 1e12 / PEAK_FP32_TFLOPS,
+            "mfma_issue_frac": (all_flop * issue / step_s / 1e12 /
+                                (PEAK_BF16_TFLOPS if args.precision == "bf16x3" else PEAK_FP32_TFLOPS)),
+            "mfma_issue_note": ("algorithmic FLOP x 3 bf16 MFMA products per multiply-add / step "
+                                "time / 2.5 PF bf16 dense peak" if args.precision == "bf16x3" else
+                                "algorithmic FLOP / step time / 157.3 TF fp32 MFMA peak"),
             "hbm_model_GBs": all_bytes / step_s / 1e9,
             "hbm_model_frac": all_bytes / step_s / 1e9 / PEAK_HBM_GBS,
             "kernel_time_ms": tot_ms,
@@ -412,9 +566,26 @@ def main():
             "note": "equivalent bandwidth of the layer-streaming model at the measured step "
                     "time; the fused kernels move fewer bytes (PMC traffic in roofline)",
         }
+        if pmc:
+            # measured HBM bytes of one step: every kernel's PMC bytes per launch x its launches
+            # per step (1-stream pass counts; the 2-stream value pass moves the same bytes)
+            meas, missing = 0.0, []
+            for k, v in prof.items():
+                if _norm(k) in pmc:
+                    meas += pmc[_norm(k)]["bytes"] * v["launches"] / args.steps
+                else:
+                    missing.append(k)
+            line["roofline_step"]["hbm_pmc"] = {
+                "bytes_per_step": meas, "GBs": meas / step_s / 1e9,
+                "frac": meas / step_s / 1e9 / PEAK_HBM_GBS,
+                "kernels_without_pmc": missing,
+                "note": "measured: sum of per-kernel PMC bytes per step / value-pass step time"}
         line["kernels"] = {k: {"launches": v["launches"] // args.steps,
                                "ms_per_step": v["ms"] / args.steps,
-                               "TFLOPs": v["flop"] / (v["ms"] * 1e-3) / 1e12 if v["ms"] else None}
+                               "TFLOPs": v["flop"] / (v["ms"] * 1e-3) / 1e12 if v["ms"] else None,
+                           "pmc_bytes_per_launch": (pmc[_norm(k)]["bytes"]
+                                                    if pmc and _norm(k) in pmc else None),
+                           "alg_bytes_per_launch": v["bytes"] / v["launches"]}
                            for k, v in sorted(prof.items(), key=lambda kv: -kv[1]["ms"])}
     if world == 1 and not args.no_extra:
         line["extra_configs"] = extra_configs(pkg, S, dev, args.precision)

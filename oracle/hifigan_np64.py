@@ -45,7 +45,10 @@ def conv_transpose1d(x, w, b, stride, pad):
     return y[:, :, pad: pad + lout] + b[None, :, None]
 
 
-def generator_forward(sd, cfg: GenConfig, mel):
+def generator_forward(sd, cfg: GenConfig, mel, tap=None):
+    """float64 forward; ``tap(name, array)`` sees conv_pre / ups.i / mrfs.i like
+    oracle.hifigan_torch.generator_forward."""
+    tap = tap or (lambda name, t: None)
     f = {k: np.asarray(v, dtype=np.float64) for k, v in sd.items()}
     for k in list(f):
         if k.endswith(".weight_g"):
@@ -54,9 +57,11 @@ def generator_forward(sd, cfg: GenConfig, mel):
             norm = np.sqrt((v ** 2).reshape(v.shape[0], -1).sum(1)).reshape(g.shape)
             f[mod + ".weight"] = g * v / norm
     x = conv1d(np.asarray(mel, np.float64), f["conv_pre.weight"], f["conv_pre.bias"], 3, 1)
+    tap("conv_pre", x)
     n_res = len(cfg.resblock_kernel_sizes)
     for i, (u, k) in enumerate(zip(cfg.upsample_rates, cfg.upsample_kernel_sizes)):
         x = conv_transpose1d(lrelu(x), f[f"ups.{i}.weight"], f[f"ups.{i}.bias"], u, (k - u) // 2)
+        tap(f"ups.{i}", x)
         acc = 0.0
         for j, (kr, dils) in enumerate(zip(cfg.resblock_kernel_sizes, cfg.resblock_dilation_sizes)):
             xr = x
@@ -69,5 +74,6 @@ def generator_forward(sd, cfg: GenConfig, mel):
                 xr = xr + xt
             acc = acc + xr
         x = acc / n_res
+        tap(f"mrfs.{i}", x)
     wav = conv1d(lrelu(x), f["conv_post.weight"], f["conv_post.bias"], 3, 1)
     return np.tanh(wav)

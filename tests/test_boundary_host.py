@@ -101,6 +101,22 @@ def test_generator_submodules_share_reference_keys(pkg):
     assert {m.precision for m in gen.modules() if hasattr(m, "precision")} == {"bf16x3"}
 
 
+def test_load_state_dict_resets_weight_tracking(pkg):
+    """load_state_dict (on the Generator and on a sub-MRF) runs the post hooks that
+    invalidate the packed weights; torch requires those hooks to return None."""
+    import torch
+    gen = pkg.HiFiGANGenerator(**C.V2STAR.kwargs())
+    sd = {k: torch.from_numpy(v) for k, v in C.make_state_dict(C.V2STAR, seed=3).items()}
+    for m in gen.modules():
+        if hasattr(m, "_hfg_fingerprint"):
+            m._hfg_fingerprint[0] = ("stale",)
+    res = gen.load_state_dict(sd)
+    assert not res.missing_keys and not res.unexpected_keys
+    assert all(not m._hfg_fingerprint for m in gen.modules() if hasattr(m, "_hfg_fingerprint"))
+    gen.mrfs[0].load_state_dict(gen.mrfs[0].state_dict())
+    gen.mrfs[0].resblocks[1].load_state_dict(gen.mrfs[0].resblocks[1].state_dict())
+
+
 def test_package_imports_by_underscore_name():
     code = ("import tts_sambert_hifigan_amd as p, tts_sambert_hifigan_amd.glue as g; "
             "print(p.HiFiGANGenerator.__module__, os.path.basename(os.path.dirname(g.__file__)))")

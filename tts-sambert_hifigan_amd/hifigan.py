@@ -62,7 +62,12 @@ class _HipWeights(nn.Module):
         self._hfg_fingerprint: Dict[int, tuple] = {}
         self._hfg_checksum: Dict[int, torch.Tensor] = {}
         self.precision = precision
-        self.register_load_state_dict_post_hook(lambda m, _incompatible: m.refresh_weights())
+        self.register_load_state_dict_post_hook(_HipWeights._after_load)
+
+    @staticmethod
+    def _after_load(module, _incompatible_keys) -> None:
+        # torch requires load_state_dict post hooks to return None
+        module.refresh_weights()
 
     def refresh_weights(self):
         """Force a re-pack of the parameters before the next forward."""
