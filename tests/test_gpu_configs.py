@@ -136,3 +136,34 @@ def test_c5_sambert_batch32_ragged(pkg, dev, c5, precision):
         worst = max(worst, err)
         assert err < ATOL, (b, err)
     print(f"\nC5 [{precision}] 32 utterances, frames {min(lens)}-{max(lens)}: max err {worst:.2e}")
+
+
+@pytest.mark.parametrize("precision", ["bf16x3", "fp32"])
+def test_v2star_thin_stages_ragged_and_vs_layer_kernels(pkg, dev, precision):
+    """The V2* C = 16 / 8 stages run as one mrf_thin launch per MRF (csrc/mrf_thin.hip):
+    a ragged batch equals each utterance run alone (bitwise, zero past its length), and
+    the thin path agrees with the layer-per-launch kernels (HFG_THIN=0) and the oracle."""
+    from oracle import config as C, hifigan_torch as H
+    cfg = C.V2STAR
+    sd = C.make_state_dict(cfg, seed=21)
+    gen = _gen(pkg, cfg, sd, dev, precision)
+    g = torch.Generator().manual_seed(7)
+    lens = [37, 64, 5, 50]
+    mel = torch.randn(4, 80, 64, generator=g)
+    wav = _run(gen, mel.to(dev), lengths=lens)
+    for b, n in enumerate(lens):
+        solo = _run(gen, mel[b:b + 1, :, :n].contiguous().to(dev))
+        assert torch.equal(wav[b:b + 1, :, :n * 256], solo), b
+        assert not wav[b, :, n * 256:].any(), b
+        ref = H.generator_forward(H.to_torch_state(sd), cfg, mel[b:b + 1, :, :n])
+        assert (solo.cpu() - ref).abs().max().item() < ATOL, b
+    os.environ["HFG_THIN"] = "0"
+    try:
+        gen_l = _gen(pkg, cfg, sd, dev, precision)
+        wav_l = _run(gen_l, mel.to(dev))
+    finally:
+        del os.environ["HFG_THIN"]
+    wav_t = _run(gen, mel.to(dev))
+    err = (wav_t - wav_l).abs().max().item()
+    print(f"\nV2* thin vs layer kernels [{precision}]: {err:.2e}")
+    assert err < 2e-5

@@ -90,6 +90,13 @@ struct Stage {
   std::vector<int> conv1;     // [j*n_dil + m]
   std::vector<int> conv2;
   std::vector<RbFused> rbs;   // per ResBlock: whole-block launch or layer by layer
+  // thin stage (C <= 16): the whole MRF in one mrf_thin launch (packed-fp32 VALU)
+  bool thin = false;
+  std::vector<int> thin_convs;   // layer indices: conv1_0, conv2_0, conv1_1, ... per ResBlock
+  std::vector<int> thin_conv0;   // ResBlock j runs thin_convs[thin_conv0[j] .. thin_conv0[j+1])
+  std::vector<int> thin_halo;    // per ResBlock receptive-field radius
+  std::vector<size_t> thin_w_off;  // per conv, floats into the packed buffer ([tap][ci][co])
+  size_t thin_b_off = 0;           // [conv][C]
 };
 
 }  // namespace
@@ -123,6 +130,8 @@ struct hfg_handle {
   int rb_waves_n32 = 4;      // window of the C = 32 ResBlock kernel: 128 * this columns
                              // (HFG_RB_WN32: 4 or 8)
   bool mfma16 = true;        // 16x16x32-shape ResBlock kernel for C = 32 (HFG_MFMA16=0: off)
+  bool thin = true;          // whole-MRF VALU kernel for C <= 16 stages (HFG_THIN=0: layer
+                             // kernels instead)
   bool c16 = false;          // 16x16x32-shape wide layer kernel conv16_bf16x3 (HFG_C16=1;
                              // parity-green, measured 26-45% slower than tile 3 on r01)
   int dbg_flags = 0;  // HFG_DEBUG_FLAGS env (kernel ablations; wrong results when set)
@@ -391,8 +400,63 @@ int build_layers(hfg_handle* h) {
       st.rbs[j] = std::move(rb);
     }
   }
+  // thin stages (C <= 16, both precisions): one mrf_thin launch per MRF
+  for (auto& st : h->stages) {
+    const int C = st.C;
+    const int nwin = hfg::thin_window(C);
+    if (!h->thin || nwin == 0 || c.n_res > hfg::kThinMaxRes) continue;
+    int n_conv = 0, halo_max = 0;
+    bool ok = true;
+    std::vector<int> convs, conv0, halos;
+    int idx = 0;
+    for (int j = 0; j < c.n_res; ++j) {
+      conv0.push_back((int)convs.size());
+      int halo = 0;
+      for (int m = 0; m < c.n_dil[j]; ++m, ++idx) {
+        convs.push_back(st.conv1[idx]);
+        convs.push_back(st.conv2[idx]);
+        const int kr = c.res_kernels[j];
+        if ((kr - 1) / 2 * c.dil[j][m] > hfg::kThinMarg) ok = false;
+        halo += (kr - 1) / 2 * c.dil[j][m] + (kr - 1) / 2;
+      }
+      halos.push_back(halo);
+      halo_max = std::max(halo_max, halo);
+    }
+    conv0.push_back((int)convs.size());
+    n_conv = (int)convs.size();
+    if (n_conv > hfg::kThinMaxConv || nwin - 2 * halo_max < nwin / 4) ok = false;
+    if (!ok) continue;
+    st.thin = true;
+    st.thin_convs = convs;
+    st.thin_conv0 = conv0;
+    st.thin_halo = halos;
+    st.thin_w_off.clear();
+    for (int cv : convs) {
+      st.thin_w_off.push_back(off);
+      off += ((size_t)h->layers[cv].k * C * C + 63) & ~(size_t)63;
+    }
+    st.thin_b_off = off;
+    off += ((size_t)n_conv * C + 63) & ~(size_t)63;
+  }
   h->packed_host.assign(off, 0.f);
   return HFG_OK;
+}
+
+// mrf_thin weights: per conv [tap][ci][co] fp32 (the C output channels of one (tap, ci)
+// are one scalar load), biases [conv][C]
+void pack_thin(hfg_handle* h, const Stage& st) {
+  const int C = st.C;
+  for (size_t e = 0; e < st.thin_convs.size(); ++e) {
+    const Layer& L = h->layers[st.thin_convs[e]];
+    const float* w = h->params[L.mod + ".weight"].data.data();  // [C_out][C_in][k]
+    float* dst = h->packed_host.data() + st.thin_w_off[e];
+    for (int j = 0; j < L.k; ++j)
+      for (int ci = 0; ci < C; ++ci)
+        for (int co = 0; co < C; ++co)
+          dst[((size_t)j * C + ci) * C + co] = w[((size_t)co * C + ci) * L.k + j];
+    const float* bsrc = h->params[L.mod + ".bias"].data.data();
+    for (int co = 0; co < C; ++co) h->packed_host[st.thin_b_off + e * C + co] = bsrc[co];
+  }
 }
 
 // Fragment order of conv1d_mfma_f32's A operand (see conv_kernels.hip):
@@ -661,9 +725,11 @@ int do_commit(hfg_handle* h) {
     if (!h->params[key].set) return fail(HFG_EAGAIN, "weight '%s' was never set", key.c_str());
   std::fill(h->packed_host.begin(), h->packed_host.end(), 0.f);
   for (auto& L : h->layers) pack_layer(h, L);
-  for (auto& st : h->stages)
+  for (auto& st : h->stages) {
     for (auto& rb : st.rbs)
       if (rb.fused) pack_resblock(h, rb);
+    if (st.thin) pack_thin(h, st);
+  }
   if (h->device >= 0) {
     DeviceGuard g(h->device);
     if (!g.ok) return fail(HFG_ENODEV, "hipSetDevice(%d) failed", h->device);
@@ -920,12 +986,59 @@ int run_ups(hfg_handle* h, Launcher& ln, const Layer& L, const float* x, int64_t
   return HFG_OK;
 }
 
+// A thin stage's whole MRF (or ResBlock only_j alone) in one mrf_thin launch.
+int run_thin(hfg_handle* h, Launcher& ln, const Stage& st, const float* X, int64_t B, int64_t Lt,
+             float* out, const int32_t* lens, int only_j) {
+  const hfg_config& c = h->cfg;
+  const int C = st.C;
+  hfg::ThinParams p{};
+  p.x = X;
+  p.bs = (int64_t)C * Lt;
+  p.L = (int)Lt;
+  p.len = lens;
+  p.w = h->packed_dev;
+  p.bias = h->packed_dev + st.thin_b_off;
+  const int j0 = only_j >= 0 ? only_j : 0, j1 = only_j >= 0 ? only_j + 1 : c.n_res;
+  p.n_res = j1 - j0;
+  const int cv_base = st.thin_conv0[j0];
+  double flop = 0.0, wbytes = 0.0;
+  int halo = 0;
+  for (int j = j0; j < j1; ++j) {
+    p.rb_conv0[j - j0] = st.thin_conv0[j] - cv_base;
+    halo = std::max(halo, st.thin_halo[j]);
+  }
+  p.rb_conv0[p.n_res] = st.thin_conv0[j1] - cv_base;
+  for (int e = st.thin_conv0[j0]; e < st.thin_conv0[j1]; ++e) {
+    const Layer& L = h->layers[st.thin_convs[e]];
+    const int q = e - cv_base;
+    p.kt[q] = L.k;
+    p.dil[q] = L.dil;
+    p.w_off[q] = (int)st.thin_w_off[e];
+    flop += 2.0 * C * C * L.k * (double)Lt * B;
+    wbytes += 4.0 * C * C * L.k;
+  }
+  // the kernel indexes biases as [conv][C] from this launch's first conv
+  p.bias = h->packed_dev + st.thin_b_off + (size_t)cv_base * C;
+  p.halo = halo;
+  p.W = hfg::thin_window(C) - 2 * halo;
+  p.y = out;
+  p.div = (float)p.n_res;
+  const double bytes = 8.0 * B * Lt * C + wbytes;  // x once, y once, weights once
+  const char* name = nullptr;
+  ln.begin(flop, bytes);
+  hipError_t e = hfg::launch_mrf_thin(C, p, (int)B, ln.stream, &name);
+  ln.end(name);
+  if (e != hipSuccess) return fail(HFG_EIO, "launch mrf_thin (C=%d): %s", C, hipGetErrorString(e));
+  return HFG_OK;
+}
+
 // MRF of stage st (models/hifigan.py:116-131) on X [B][C][L]: out = mean_j ResBlock_j(X)
 // (ResBlock.forward :72-86), or out = ResBlock_only_j(X) alone when only_j >= 0.  R and Tb
 // are B*C*L-float scratch buffers of the layer-per-launch ResBlocks; out must not alias X.
 int run_mrf(hfg_handle* h, Launcher& ln, const Stage& st, const float* X, int64_t B, int64_t L,
             float* R, float* Tb, float* out, const int32_t* lens, int only_j) {
   const hfg_config& c = h->cfg;
+  if (st.thin) return run_thin(h, ln, st, X, B, L, out, lens, only_j);
   int rc;
   int idx = 0;
   for (int j = 0; j < c.n_res; ++j) {
@@ -1111,6 +1224,7 @@ int create_impl(const hfg_config* cfg, bool mrf_only, int device, hfg_handle** o
   }
   if (const char* fe = getenv("HFG_FUSED_RB")) h->use_fused_rb = atoi(fe) != 0;
   if (const char* me = getenv("HFG_MFMA16")) h->mfma16 = atoi(me) != 0;
+  if (const char* te = getenv("HFG_THIN")) h->thin = atoi(te) != 0;
   if (const char* ce = getenv("HFG_C16")) h->c16 = atoi(ce) != 0;
   if (const char* se = getenv("HFG_SPLIT")) h->split = atoi(se);
   if (const char* rn = getenv("HFG_RB64_NARROW")) h->rb64_narrow = atoi(rn) != 0;

@@ -182,6 +182,31 @@ bool rb16_supported(int C, int kt, int waves_n);
 hipError_t launch_resblock16_bf16x3(int C, int waves_n, int kt, const RbParams& p, int batch,
                                     hipStream_t stream, const char** name);
 
+// ---- whole MRF per launch for thin stages, C <= 16 (mrf_thin.hip) ----
+// All ResBlocks of one MRF on a time window in LDS, packed-fp32 VALU dot products (exact
+// fp32 products).  Weights packed per conv [tap][ci][co] (fp32), biases [conv][C].
+constexpr int kThinMarg = 64;      // spare operand columns per side: every (k-1)/2*d must fit
+constexpr int kThinMaxRes = 8;
+constexpr int kThinMaxConv = 64;
+struct ThinParams {
+  const float* x;            // stage input [B][C][L]
+  int64_t bs;                // batch stride of x and y (C * L)
+  int L;
+  const int32_t* len;        // per-item valid length (device, [B]) or null = L
+  const float* w;            // packed weights (floats)
+  const float* bias;         // [conv][C]
+  int n_res;                 // ResBlocks in this launch
+  int rb_conv0[kThinMaxRes + 1];  // ResBlock r runs convs [rb_conv0[r], rb_conv0[r+1])
+  int kt[kThinMaxConv], dil[kThinMaxConv], w_off[kThinMaxConv];  // per conv (conv1, conv2, ...)
+  int halo, W;               // largest ResBlock radius, output columns per block
+  float* y;                  // [B][C][L] <- (sum of the ResBlocks' outputs) / div
+  float div;
+};
+int thin_window(int C);      // window columns of the C-channel instance (0: unsupported C)
+size_t thin_lds_bytes(int C);
+hipError_t launch_mrf_thin(int C, const ThinParams& p, int batch, hipStream_t stream,
+                           const char** name);
+
 // Launch the conv kernel for (tile, taps, ups).  Returns a hipError_t and,
 // via *name, the kernel's template-instance name (as rocprofv3 prints it).
 hipError_t launch_conv(TileId tile, int kt, bool ups, const ConvParams& p, int n_tiles,
