@@ -61,17 +61,19 @@ extern "C" {
 #define HFG_EAGAIN (-11)   /* weights incomplete (a key was never set)    */
 #define HFG_EIO (-5)       /* HIP runtime error (launch, memcpy, ...)     */
 
-/* Arithmetic of the Generator's convolutions (conv_post + tanh always runs in
- * exact fp32 on the vector ALUs).
+/* Arithmetic of the Generator's convolutions.  In both modes conv_post + tanh and
+ * the MRFs of thin stages (C <= 16 channels, e.g. V2*'s last two: one mrf_thin launch
+ * per MRF on the packed-fp32 vector ALUs) compute exact fp32 products.
  *   FP32   : fp32 operands on the fp32 matrix cores (v_mfma_f32_32x32x2_f32),
- *            exact fp32 products (the parity reference mode), every conv.
+ *            exact fp32 products (the parity reference mode), every other conv.
  *   BF16X3 : every fp32 operand split as hi = bf16(v), lo = bf16(v - hi);
  *            hi*hi + hi*lo + lo*hi accumulated in fp32 on the bf16 matrix cores
- *            (~16-bit-mantissa products, 5.3x the fp32 MFMA rate): conv_pre, the
- *            upsamplers and every ResBlock conv whose GEMM has >= 32 rows and whose
- *            (k-1)*dilation fits the kernels' window; the rest (e.g. the 16- and
- *            8-channel stages of narrow configs) on the fp32 kernels.  Output
- *            within ~1e-5 of the reference at default weight scale (1e-4 bar). */
+ *            (~16-bit-mantissa products, 5.3x the fp32 MFMA rate): conv_pre, every
+ *            upsampler whose polyphase GEMM has >= 32 rows (all four in V1), the
+ *            whole-ResBlock kernels of the C = 32/64/128 stages and the layer convs
+ *            of C >= 32; convs whose (k-1)*dilation exceeds the bf16x3 window fall
+ *            back to the fp32 kernels.  Output within ~1e-5 of the reference at
+ *            default weight scale (1e-4 bar; DESIGN.md §4 gives the x4-scale limit). */
 #define HFG_DTYPE_FP32 0
 #define HFG_DTYPE_BF16X3 1
 

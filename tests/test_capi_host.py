@@ -220,7 +220,8 @@ def test_bf16x3_packing(pkg, preset, big_tile, monkeypatch):
     for k, v in sd.items():
         h.set_weight(k, torch.from_numpy(v))
     h.commit()
-    WAVES = {0: (2, 2, 4), 1: (1, 2, 2), 2: (1, 1, 4), 3: (2, 2, 2)}  # tile -> (WAVES_M, WM, TPC)
+    # tile -> (WAVES_M, WM, TPC); ids 8 / 9 are conv_ws_bf16x3 / conv16_bf16x3 (kernels.h)
+    WAVES = {0: (2, 2, 4), 1: (1, 2, 2), 2: (1, 1, 4), 3: (2, 2, 2), 4: (2, 1, 4)}
     n_checked = 0
     for mod in ["conv_pre", "mrfs.0.resblocks.2.convs1.1", "mrfs.1.resblocks.0.convs2.1",
                 "mrfs.2.resblocks.1.convs1.0", "mrfs.3.resblocks.2.convs2.1"]:
@@ -231,8 +232,8 @@ def test_bf16x3_packing(pkg, preset, big_tile, monkeypatch):
             assert cout < 32
             continue
         n_checked += 1
-        if info["tile"] in (4, 5):
-            rec = (unpack_ws if info["tile"] == 4 else unpack_c16)(info, packed)[:cout, :cin, :k]
+        if info["tile"] in (8, 9):
+            rec = (unpack_ws if info["tile"] == 8 else unpack_c16)(info, packed)[:cout, :cin, :k]
             assert np.abs(rec - W).max() / np.abs(W).max() < 2.0 ** -15, mod
             assert np.array_equal(bias[:cout], sd[mod + ".bias"])
             continue
@@ -307,9 +308,9 @@ def unpack_c16(info, packed):
 
 def unpack_bf16x3(info, packed, waves):
     """Invert conv_bf16x3's fragment order → Wt[row][ci][tap] (hi + lo, float64)."""
-    if info["tile"] == 4:
+    if info["tile"] == 8:
         return unpack_ws(info, packed)
-    if info["tile"] == 5:
+    if info["tile"] == 9:
         return unpack_c16(info, packed)
     wm_, WM, TPC = waves
     MT = info["MT"]
@@ -342,7 +343,7 @@ def test_bf16x3_polyphase_upsampler_packing(pkg, c16, monkeypatch):
     for k, v in sd.items():
         h.set_weight(k, torch.from_numpy(v))
     h.commit()
-    waves = {0: (2, 2, 4), 1: (1, 2, 2), 2: (1, 1, 4), 3: (2, 2, 2), 4: None, 5: None}
+    waves = {0: (2, 2, 4), 1: (1, 2, 2), 2: (1, 1, 4), 3: (2, 2, 2), 4: (2, 1, 4), 8: None, 9: None}
     rng = np.random.default_rng(1)
     c0 = cfg.upsample_initial_channel
     for i, (u, k) in enumerate(zip(cfg.upsample_rates, cfg.upsample_kernel_sizes)):

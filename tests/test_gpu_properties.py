@@ -180,8 +180,12 @@ def test_profiling_summary(pkg, v1, dev):
     run(gen, torch.randn(1, 80, 64, device=dev))
     h.set_profiling(False)
     prof = h.profile_summary()
-    assert sum(v["launches"] for v in prof.values()) == 78
-    assert all(v["ms"] > 0 for v in prof.values())
+    # 78 conv launches; a small forward runs its MRFs' ResBlocks on concurrent streams and
+    # adds one mrf_combine launch per such stage (hifigan_capi.cpp run_mrf)
+    combine = prof.get("mrf_combine", {"launches": 0})["launches"]
+    assert sum(v["launches"] for v in prof.values()) - combine == 78
+    assert combine <= 4
+    assert all(v["ms"] > 0 for k, v in prof.items() if k != "mrf_combine")
     from oracle import config as C
     total_flop = sum(v["flop"] for v in prof.values())
     assert abs(total_flop - 2398848 * 64 * 256) / total_flop < 1e-5  # summary prints 7 digits

@@ -513,8 +513,9 @@ struct Entry3 {
 
 #define HFG3_ENTRY(KT, TILE, UPS) \
   { KT, TILE, UPS, Inst3<KT, TILE, UPS>::fn(), false, {0} }
-#define HFG3_TILES(KT, UPS) \
-  HFG3_ENTRY(KT, 0, UPS), HFG3_ENTRY(KT, 1, UPS), HFG3_ENTRY(KT, 2, UPS), HFG3_ENTRY(KT, 3, UPS)
+#define HFG3_TILES(KT, UPS)                                                              \
+  HFG3_ENTRY(KT, 0, UPS), HFG3_ENTRY(KT, 1, UPS), HFG3_ENTRY(KT, 2, UPS), HFG3_ENTRY(KT, 3, UPS), \
+      HFG3_ENTRY(KT, 4, UPS)
 
 Entry3 g_entries3[] = {
     HFG3_TILES(3, false), HFG3_TILES(5, false), HFG3_TILES(7, false), HFG3_TILES(11, false),

@@ -26,6 +26,8 @@
 // an HBM-bound reduction over C*7 inputs per sample, LDS-staged.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include <cstdio>
 
 #include "epilogue.h"
@@ -398,6 +400,51 @@ __global__ void stage_lengths_kernel(const int32_t* __restrict__ lens, int B, St
 hipError_t launch_stage_lengths(const int32_t* lens, int B, const StageLenParams& sp,
                                 int32_t* out, hipStream_t stream) {
   stage_lengths_kernel<<<dim3((B + 255) / 256), dim3(256), 0, stream>>>(lens, B, sp, out);
+  return hipGetLastError();
+}
+
+// MRF mean of ResBlock outputs computed on concurrent streams (models/hifigan.py:125-131):
+// y = (((o_0 + o_1) + o_2) + ...) / n, the same additions in the same order as the
+// sequential schedule's epilogue running sum, so the result is bitwise the same.
+// float4 over [B][C][L] rows (L % 4 == 0) with a scalar tail; columns past len[b] skipped.
+__global__ void __launch_bounds__(256) mrf_combine_kernel(MrfCombineArgs a) {
+  const int b = blockIdx.y;
+  const int len_b = a.len ? min(a.len[b], a.L) : a.L;
+  const int64_t base = (int64_t)b * a.C * a.L;
+  const int64_t n = (int64_t)a.C * a.L;
+  for (int64_t i = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4; i < n;
+       i += (int64_t)gridDim.x * 256 * 4) {
+    const int t = (int)(i % a.L);
+    if (t >= len_b) continue;
+    if ((a.L & 3) == 0) {
+      float4 acc = *reinterpret_cast<const float4*>(a.o[0] + base + i);
+      for (int j = 1; j < a.n; ++j) {
+        const float4 v = *reinterpret_cast<const float4*>(a.o[j] + base + i);
+        acc.x = acc.x + v.x;
+        acc.y = acc.y + v.y;
+        acc.z = acc.z + v.z;
+        acc.w = acc.w + v.w;
+      }
+      acc.x = acc.x / a.div;
+      acc.y = acc.y / a.div;
+      acc.z = acc.z / a.div;
+      acc.w = acc.w / a.div;
+      *reinterpret_cast<float4*>(a.y + base + i) = acc;
+    } else {
+      for (int e = 0; e < 4 && i + e < n; ++e) {
+        float acc = a.o[0][base + i + e];
+        for (int j = 1; j < a.n; ++j) acc = acc + a.o[j][base + i + e];
+        a.y[base + i + e] = acc / a.div;
+      }
+    }
+  }
+}
+
+hipError_t launch_mrf_combine(const MrfCombineArgs& a, int batch, hipStream_t stream) {
+  if (a.n < 1 || a.n > kMrfCombineMax) return hipErrorInvalidValue;
+  const int64_t n4 = ((int64_t)a.C * a.L + 3) / 4;
+  const int gx = (int)std::min<int64_t>((n4 + 255) / 256, 4096);
+  mrf_combine_kernel<<<dim3(gx, batch), dim3(256), 0, stream>>>(a);
   return hipGetLastError();
 }
 

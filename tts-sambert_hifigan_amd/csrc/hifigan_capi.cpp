@@ -59,6 +59,9 @@ struct Layer {
   int prec;          // 0: fp32 MFMA kernel, 1: bf16x3 split-precision kernel
   size_t w_off, b_off;  // offsets (floats) into the packed device buffer
   size_t w_len, b_len;
+  // bf16x3 layers: a second packing for the small-grid tile (kBf16x3SmallTile), -1: none
+  int tile_s = -1, m_tiles_s = 0, n_chunks_s = 0;
+  size_t ws_off = 0, bs_off = 0;
 };
 
 struct Param {
@@ -130,6 +133,8 @@ struct hfg_handle {
   int rb_waves_n32 = 4;      // window of the C = 32 ResBlock kernel: 128 * this columns
                              // (HFG_RB_WN32: 4 or 8)
   bool mfma16 = true;        // 16x16x32-shape ResBlock kernel for C = 32 (HFG_MFMA16=0: off)
+  int small_tile = -1;       // small-grid tile: -1 auto (grid < kSmallGridBlocks), 0 never,
+                             // 1 always (HFG_SMALL_TILE)
   bool thin = true;          // whole-MRF VALU kernel for C <= 16 stages (HFG_THIN=0: layer
                              // kernels instead)
   bool c16 = false;          // 16x16x32-shape wide layer kernel conv16_bf16x3 (HFG_C16=1;
@@ -140,6 +145,12 @@ struct hfg_handle {
   int split = 2;
   hipStream_t aux = nullptr;
   hipEvent_t fork_ev = nullptr, join_ev = nullptr;
+  // concurrent ResBlocks of small forwards (HFG_RB_CONC: -1 auto, 0 off, 1 whenever the
+  // workspace allows): per batch part, aux streams for ResBlocks 1.. and their events
+  int rb_conc = -1;
+  hipStream_t rb_aux[2][HFG_MAX_RES] = {};
+  hipEvent_t rb_fork[2] = {};
+  hipEvent_t rb_join[2][HFG_MAX_RES] = {};
   int fwd_count = 0;
   std::vector<ProfRec> prof;
   std::vector<hipEvent_t> event_pool;
@@ -338,6 +349,17 @@ int build_layers(hfg_handle* h) {
       L.b_off = off;
       L.b_len = (size_t)L.m_tiles * t3.MT();
       off += (L.b_len + 63) & ~(size_t)63;
+      if (L.tile != hfg::kBf16x3SmallTile && L.M >= 64) {
+        const hfg::Bf16x3Cfg& ts = hfg::kBf16x3Tiles[hfg::kBf16x3SmallTile];
+        L.tile_s = hfg::kBf16x3SmallTile;
+        L.m_tiles_s = (L.M + ts.MT() - 1) / ts.MT();
+        L.n_chunks_s = ((L.C_in + L.CK - 1) / L.CK) * ((L.KT + ts.TPC - 1) / ts.TPC);
+        L.ws_off = off;
+        off += ((size_t)L.m_tiles_s * L.n_chunks_s * ts.TPC * 2 * ts.MT() * 16 / 2 + 63) &
+               ~(size_t)63;
+        L.bs_off = off;
+        off += ((size_t)L.m_tiles_s * ts.MT() + 63) & ~(size_t)63;
+      }
       continue;
     }
     L.prec = 0;
@@ -678,23 +700,37 @@ void pack_layer(hfg_handle* h, const Layer& L) {
     for (size_t m = 0; m < L.b_len; ++m) bdst[m] = m < (size_t)L.M ? Bp.data[m / s] : 0.f;
     return;
   }
-  if (L.kind == L_CONV && L.prec == 1) {
-    const int cin = L.C_in, k = L.k;
-    pack_bf16x3(L, [&](int row, int ci, int j) { return w[((size_t)row * cin + ci) * k + j]; },
-                reinterpret_cast<uint16_t*>(dst));
-    for (size_t m = 0; m < L.b_len; ++m) bdst[m] = m < (size_t)L.M ? Bp.data[m] : 0.f;
-    return;
-  }
-  if (L.kind == L_UPS && L.prec == 1) {
-    const int s = L.s, Q = L.KT, k = L.k, cout = L.C_out;
-    pack_bf16x3(L,
-                [&](int row, int ci, int jj) {
-                  const int co = row / s, r = row % s;
-                  const int kidx = r + s * (Q - 1 - jj);
-                  return kidx < k ? w[((size_t)ci * cout + co) * k + kidx] : 0.f;
-                },
-                reinterpret_cast<uint16_t*>(dst));
-    for (size_t m = 0; m < L.b_len; ++m) bdst[m] = m < (size_t)L.M ? Bp.data[m / s] : 0.f;
+  if (L.prec == 1 && (L.kind == L_CONV || L.kind == L_UPS)) {
+    // the layer's tile, then (bf16x3 layers with a small-grid packing) the small tile
+    for (int pass = 0; pass < (L.tile_s >= 0 ? 2 : 1); ++pass) {
+      Layer Lp = L;
+      float* wd = dst;
+      float* bd = bdst;
+      if (pass == 1) {
+        Lp.tile = L.tile_s;
+        Lp.m_tiles = L.m_tiles_s;
+        Lp.n_chunks = L.n_chunks_s;
+        Lp.b_len = (size_t)L.m_tiles_s * hfg::kBf16x3Tiles[L.tile_s].MT();
+        wd = h->packed_host.data() + L.ws_off;
+        bd = h->packed_host.data() + L.bs_off;
+      }
+      if (L.kind == L_CONV) {
+        const int cin = L.C_in, k = L.k;
+        pack_bf16x3(Lp, [&](int row, int ci, int j) { return w[((size_t)row * cin + ci) * k + j]; },
+                    reinterpret_cast<uint16_t*>(wd));
+        for (size_t m = 0; m < Lp.b_len; ++m) bd[m] = m < (size_t)L.M ? Bp.data[m] : 0.f;
+      } else {
+        const int s = L.s, Q = L.KT, k = L.k, cout = L.C_out;
+        pack_bf16x3(Lp,
+                    [&](int row, int ci, int jj) {
+                      const int co = row / s, r = row % s;
+                      const int kidx = r + s * (Q - 1 - jj);
+                      return kidx < k ? w[((size_t)ci * cout + co) * k + kidx] : 0.f;
+                    },
+                    reinterpret_cast<uint16_t*>(wd));
+        for (size_t m = 0; m < Lp.b_len; ++m) bd[m] = m < (size_t)L.M ? Bp.data[m / s] : 0.f;
+      }
+    }
     return;
   }
   if (L.kind == L_CONV) {
@@ -780,9 +816,31 @@ Shapes shapes_for(const hfg_handle* h, int64_t B, int64_t T) {
 size_t lens_table_bytes(const hfg_handle* h, int64_t B) {
   return (((size_t)(h->cfg.n_up + 1) * (size_t)B * sizeof(int32_t)) + 255) & ~(size_t)255;
 }
+// concurrent ResBlocks for a stage whose layer grids leave CUs idle: fewer tile-3 blocks
+// (128 rows x 256 columns) per conv than the chip's 512 slots
+bool stage_conc(const hfg_handle* h, const Stage& st, int64_t B, int64_t L) {
+  const int n_res = h->cfg.n_res;
+  if (h->rb_conc == 0 || st.thin || n_res < 2 || n_res > hfg::kMrfCombineMax) return false;
+  if (h->rb_conc == 1) return true;
+  return B * ((L + 255) / 256) * ((st.C + 127) / 128) < 512;
+}
+bool any_conc(const hfg_handle* h, int64_t B, int64_t T) {
+  if (h->mrf_only) return false;
+  const Shapes sh = shapes_for(h, B, T);
+  for (size_t i = 0; i < h->stages.size(); ++i)
+    if (stage_conc(h, h->stages[i], B, sh.L[i + 1])) return true;
+  return false;
+}
+// activation buffers of one forward_impl call: X, R, Tb, MRF, and with concurrent
+// ResBlocks an R / Tb / output triple per ResBlock
+int n_bufs(const hfg_handle* h, int64_t B, int64_t T, bool conc_ok) {
+  return 4 + (conc_ok && any_conc(h, B, T) ? 3 * h->cfg.n_res : 0);
+}
 // workspace of one forward_impl call (one batch half)
-size_t ws_part_bytes(const hfg_handle* h, int64_t B, int64_t T) {
-  const size_t n = 4 * sizeof(float) * (size_t)shapes_for(h, B, T).buf_elems + lens_table_bytes(h, B);
+size_t ws_part_bytes(const hfg_handle* h, int64_t B, int64_t T, bool conc_ok = false) {
+  const size_t n = (size_t)n_bufs(h, B, T, conc_ok) * sizeof(float) *
+                       (size_t)shapes_for(h, B, T).buf_elems +
+                   lens_table_bytes(h, B);
   return (n + 255) & ~(size_t)255;
 }
 // small forwards stay on one stream: splitting them doubles an already latency-bound
@@ -791,9 +849,10 @@ constexpr int64_t kSplitMinFrames = 4096;
 bool split_batch(const hfg_handle* h, int64_t B, int64_t T) {
   return h->split >= 2 && B >= 2 && B * T >= kSplitMinFrames;
 }
-// workspace of a forward: both halves' when the batch is split over two streams
+// workspace of a forward: both halves' when the batch is split over two streams (whose
+// ResBlocks then run one after another), else one part with concurrent ResBlocks allowed
 size_t ws_bytes_for(const hfg_handle* h, int64_t B, int64_t T) {
-  if (!split_batch(h, B, T)) return ws_part_bytes(h, B, T);
+  if (!split_batch(h, B, T)) return ws_part_bytes(h, B, T, true);
   const int64_t B1 = (B + 1) / 2;
   return ws_part_bytes(h, B1, T) + ws_part_bytes(h, B - B1, T);
 }
@@ -822,6 +881,7 @@ struct Launcher {
   hipStream_t stream;
   int part = 0;
   int seq = 0;
+  int conc = 1;  // launches of this schedule running side by side (concurrent ResBlocks)
   ProfRec* rec = nullptr;
   void begin(double flop, double bytes) {
     rec = nullptr;
@@ -837,6 +897,29 @@ struct Launcher {
     if (rec->e1) (void)hipEventRecord(rec->e1, stream);
   }
 };
+
+// Small-grid switch of a bf16x3 layer launch: when the layer's tile leaves most CUs idle
+// (fewer than kSmallGridBlocks blocks), run the small tile on its own packing.  Bitwise
+// the same result (kernels.h, tile 4).  Updates p's weights / chunks; returns the tile.
+int pick_tile(const hfg_handle* h, const Layer& L, hfg::ConvParams& p, int64_t n_cols, int64_t B,
+              int conc, int& n_tiles, int& m_tiles) {
+  int tile = L.tile;
+  m_tiles = L.m_tiles;
+  if (L.prec != 1 || L.tile_s < 0 || L.tile == hfg::kWsTile || L.tile == hfg::kC16Tile ||
+      h->small_tile == 0)
+    return tile;
+  // conc: the grids of that many concurrent launches share the chip
+  const bool small =
+      h->small_tile == 1 || (int64_t)n_tiles * m_tiles * B * conc < hfg::kSmallGridBlocks;
+  if (!small) return tile;
+  tile = L.tile_s;
+  m_tiles = L.m_tiles_s;
+  n_tiles = (int)((n_cols + hfg::kBf16x3Tiles[tile].NTILE() - 1) / hfg::kBf16x3Tiles[tile].NTILE());
+  p.w = h->packed_dev + L.ws_off;
+  p.bias = h->packed_dev + L.bs_off;
+  p.n_chunks = L.n_chunks_s;
+  return tile;
+}
 
 // One conv-layer launch (regular Conv1d).
 int run_conv(hfg_handle* h, Launcher& ln, const Layer& L, const float* x, int64_t B, int64_t Lt,
@@ -872,7 +955,8 @@ int run_conv(hfg_handle* h, Launcher& ln, const Layer& L, const float* x, int64_
                     : L.tile == hfg::kC16Tile ? hfg::kC16NT
                     : L.prec == 1             ? hfg::kBf16x3Tiles[L.tile].NTILE()
                                               : kTiles[L.tile].NTILE();
-  const int n_tiles = (int)((Lt + ntile - 1) / ntile);
+  int n_tiles = (int)((Lt + ntile - 1) / ntile), m_tiles = L.m_tiles;
+  const int tile = pick_tile(h, L, p, Lt, B, ln.conc, n_tiles, m_tiles);
   const double flop = 2.0 * L.C_out * L.C_in * L.k * (double)Lt * B;
   double bytes = 4.0 * B * Lt * (L.C_in + L.C_out) + 4.0 * L.C_out * L.C_in * L.k;
   if (res) bytes += 4.0 * B * Lt * L.C_out;
@@ -886,7 +970,7 @@ int run_conv(hfg_handle* h, Launcher& ln, const Layer& L, const float* x, int64_
                      ? hfg::launch_conv16_bf16x3(L.KT, false, p, n_tiles, L.m_tiles, (int)B,
                                                  ln.stream, &name)
                  : L.prec == 1
-                     ? hfg::launch_conv_bf16x3(L.tile, L.KT, false, p, n_tiles, L.m_tiles, (int)B,
+                     ? hfg::launch_conv_bf16x3(tile, L.KT, false, p, n_tiles, m_tiles, (int)B,
                                                ln.stream, &name)
                      : hfg::launch_conv((TileId)L.tile, L.KT, false, p, n_tiles, L.m_tiles,
                                         (int)B, ln.stream, &name);
@@ -965,7 +1049,8 @@ int run_ups(hfg_handle* h, Launcher& ln, const Layer& L, const float* x, int64_t
                     : L.tile == hfg::kC16Tile ? hfg::kC16NT
                     : L.prec == 1             ? hfg::kBf16x3Tiles[L.tile].NTILE()
                                               : kTiles[L.tile].NTILE();
-  const int n_tiles = (p.N + ntile - 1) / ntile;
+  int n_tiles = (p.N + ntile - 1) / ntile, m_tiles = L.m_tiles;
+  const int tile = pick_tile(h, L, p, p.N, B, ln.conc, n_tiles, m_tiles);
   const double flop = 2.0 * L.C_in * L.C_out * L.k * (double)Lin * B;
   const double bytes = 4.0 * B * (L.C_in * Lin + L.C_out * Lout) + 4.0 * L.C_in * L.C_out * L.k;
   const char* name = nullptr;
@@ -977,7 +1062,7 @@ int run_ups(hfg_handle* h, Launcher& ln, const Layer& L, const float* x, int64_t
                      ? hfg::launch_conv16_bf16x3(L.KT, true, p, n_tiles, L.m_tiles, (int)B,
                                                  ln.stream, &name)
                  : L.prec == 1
-                     ? hfg::launch_conv_bf16x3(L.tile, L.KT, true, p, n_tiles, L.m_tiles, (int)B,
+                     ? hfg::launch_conv_bf16x3(tile, L.KT, true, p, n_tiles, m_tiles, (int)B,
                                                ln.stream, &name)
                      : hfg::launch_conv((TileId)L.tile, L.KT, true, p, n_tiles, L.m_tiles, (int)B,
                                         ln.stream, &name);
@@ -1035,11 +1120,101 @@ int run_thin(hfg_handle* h, Launcher& ln, const Stage& st, const float* X, int64
 // MRF of stage st (models/hifigan.py:116-131) on X [B][C][L]: out = mean_j ResBlock_j(X)
 // (ResBlock.forward :72-86), or out = ResBlock_only_j(X) alone when only_j >= 0.  R and Tb
 // are B*C*L-float scratch buffers of the layer-per-launch ResBlocks; out must not alias X.
+// ResBlock j of stage st (ResBlock.forward, models/hifigan.py:72-86) on X, its result
+// combined into out by the MRF epilogue mode (bit0 add, bit1 divide by n_res); idx = index
+// of its first dilation in st.conv1 / st.conv2.  R, Tb: scratch of the layer-per-launch path.
+int run_one_rb(hfg_handle* h, Launcher& ln, const Stage& st, int j, int idx, const float* X,
+               int64_t B, int64_t L, float* R, float* Tb, float* out, int mode,
+               const int32_t* lens) {
+  const hfg_config& c = h->cfg;
+  if (st.rbs[j].fused) return run_resblock(h, ln, st.rbs[j], X, B, L, out, mode, (float)c.n_res, lens);
+  int rc;
+  for (int m = 0; m < c.n_dil[j]; ++m, ++idx) {
+    const float* src = (m == 0) ? X : R;
+    const Layer& L1 = h->layers[st.conv1[idx]];
+    const Layer& L2 = h->layers[st.conv2[idx]];
+    // xt = lrelu(conv1(lrelu(x)))
+    rc = run_conv(h, ln, L1, src, B, L, Tb, true, true, nullptr, nullptr, 0, 1.f, lens);
+    if (rc) return rc;
+    if (m < c.n_dil[j] - 1) {
+      // x = x + conv2(xt)
+      rc = run_conv(h, ln, L2, Tb, B, L, R, false, false, src, nullptr, 0, 1.f, lens);
+    } else {
+      rc = run_conv(h, ln, L2, Tb, B, L, nullptr, false, false, src, out, mode, (float)c.n_res,
+                    lens);
+    }
+    if (rc) return rc;
+  }
+  return HFG_OK;
+}
+
+// Scratch of the concurrent-ResBlock schedule: per ResBlock its R / Tb and its output.
+struct RbConc {
+  float* R[HFG_MAX_RES];
+  float* Tb[HFG_MAX_RES];
+  float* O[HFG_MAX_RES];
+};
+
+// Aux streams of one batch part (created on first use; hipStreamNonBlocking)
+int rb_streams(hfg_handle* h, int part) {
+  for (int j = 0; j < h->cfg.n_res - 1; ++j)
+    if (!h->rb_aux[part][j]) {
+      hipError_t e = hipStreamCreateWithFlags(&h->rb_aux[part][j], hipStreamNonBlocking);
+      if (e == hipSuccess) e = hipEventCreateWithFlags(&h->rb_join[part][j], hipEventDisableTiming);
+      if (e != hipSuccess) return hip_fail(e, "create ResBlock stream");
+    }
+  if (!h->rb_fork[part]) {
+    hipError_t e = hipEventCreateWithFlags(&h->rb_fork[part], hipEventDisableTiming);
+    if (e != hipSuccess) return hip_fail(e, "create ResBlock fork event");
+  }
+  return HFG_OK;
+}
+
+// MRF of stage st (models/hifigan.py:116-131) on X [B][C][L]: out = mean_j ResBlock_j(X)
+// (ResBlock.forward :72-86), or out = ResBlock_only_j(X) alone when only_j >= 0.  R and Tb
+// are B*C*L-float scratch buffers of the layer-per-launch ResBlocks; out must not alias X.
+// With conc set, the ResBlocks run concurrently (ResBlock j > 0 on aux stream j-1 of this
+// batch part), each into its own output, and one combine launch forms the mean in the
+// sequential schedule's order — bitwise the same result, for grids that leave CUs idle.
 int run_mrf(hfg_handle* h, Launcher& ln, const Stage& st, const float* X, int64_t B, int64_t L,
-            float* R, float* Tb, float* out, const int32_t* lens, int only_j) {
+            float* R, float* Tb, float* out, const int32_t* lens, int only_j,
+            const RbConc* conc = nullptr) {
   const hfg_config& c = h->cfg;
   if (st.thin) return run_thin(h, ln, st, X, B, L, out, lens, only_j);
   int rc;
+  if (conc && only_j < 0 && c.n_res > 1) {
+    if ((rc = rb_streams(h, ln.part))) return rc;
+    hipError_t e = hipEventRecord(h->rb_fork[ln.part], ln.stream);
+    for (int j = 1; j < c.n_res && e == hipSuccess; ++j)
+      e = hipStreamWaitEvent(h->rb_aux[ln.part][j - 1], h->rb_fork[ln.part], 0);
+    if (e != hipSuccess) return hip_fail(e, "ResBlock fork");
+    int idx = 0;
+    for (int j = 0; j < c.n_res; ++j) {
+      Launcher lj{h, j == 0 ? ln.stream : h->rb_aux[ln.part][j - 1], ln.part, ln.seq, c.n_res};
+      rc = run_one_rb(h, lj, st, j, idx, X, B, L, conc->R[j], conc->Tb[j], conc->O[j], 0, lens);
+      if (rc) return rc;
+      ln.seq = lj.seq;
+      idx += c.n_dil[j];
+    }
+    for (int j = 1; j < c.n_res && e == hipSuccess; ++j) {
+      e = hipEventRecord(h->rb_join[ln.part][j - 1], h->rb_aux[ln.part][j - 1]);
+      if (e == hipSuccess) e = hipStreamWaitEvent(ln.stream, h->rb_join[ln.part][j - 1], 0);
+    }
+    if (e != hipSuccess) return hip_fail(e, "ResBlock join");
+    hfg::MrfCombineArgs a{};
+    for (int j = 0; j < c.n_res; ++j) a.o[j] = conc->O[j];
+    a.n = c.n_res;
+    a.C = st.C;
+    a.L = (int)L;
+    a.len = lens;
+    a.y = out;
+    a.div = (float)c.n_res;
+    ln.begin(0.0, 4.0 * B * L * st.C * (c.n_res + 1));
+    e = hfg::launch_mrf_combine(a, (int)B, ln.stream);
+    ln.end("mrf_combine");
+    if (e != hipSuccess) return hip_fail(e, "launch mrf_combine");
+    return HFG_OK;
+  }
   int idx = 0;
   for (int j = 0; j < c.n_res; ++j) {
     if (only_j >= 0 && j != only_j) {
@@ -1047,29 +1222,9 @@ int run_mrf(hfg_handle* h, Launcher& ln, const Stage& st, const float* X, int64_
       continue;
     }
     const int mode = only_j >= 0 ? 0 : ((j > 0 ? 1 : 0) | (j == c.n_res - 1 ? 2 : 0));
-    if (st.rbs[j].fused) {
-      rc = run_resblock(h, ln, st.rbs[j], X, B, L, out, mode, (float)c.n_res, lens);
-      if (rc) return rc;
-      idx += c.n_dil[j];
-      continue;
-    }
-    for (int m = 0; m < c.n_dil[j]; ++m, ++idx) {
-      const float* src = (m == 0) ? X : R;
-      const Layer& L1 = h->layers[st.conv1[idx]];
-      const Layer& L2 = h->layers[st.conv2[idx]];
-      // xt = lrelu(conv1(lrelu(x)))
-      rc = run_conv(h, ln, L1, src, B, L, Tb, true, true, nullptr, nullptr, 0, 1.f, lens);
-      if (rc) return rc;
-      const bool last = (m == c.n_dil[j] - 1);
-      if (!last) {
-        // x = x + conv2(xt)
-        rc = run_conv(h, ln, L2, Tb, B, L, R, false, false, src, nullptr, 0, 1.f, lens);
-      } else {
-        rc = run_conv(h, ln, L2, Tb, B, L, nullptr, false, false, src, out, mode,
-                      (float)c.n_res, lens);
-      }
-      if (rc) return rc;
-    }
+    rc = run_one_rb(h, ln, st, j, idx, X, B, L, R, Tb, out, mode, lens);
+    if (rc) return rc;
+    idx += c.n_dil[j];
   }
   return HFG_OK;
 }
@@ -1078,7 +1233,7 @@ int run_mrf(hfg_handle* h, Launcher& ln, const Stage& st, const float* X, int64_
 // output, taps[2 + 2i] <- mrfs[i] output (models/hifigan.py:238-251); NULL entries skipped.
 int forward_impl(hfg_handle* h, const float* mel, int64_t B, int64_t T, const hfg_forward_opts* o,
                  float* wav, int64_t out_len, void* ws, size_t ws_len, hipStream_t stream,
-                 int part = 0, float* const* taps = nullptr) {
+                 int part = 0, float* const* taps = nullptr, bool conc_ok = false) {
   if (!mel || !wav) return fail(HFG_EINVAL, "mel / wav pointer is NULL");
   const bool btc = o && o->mel_layout == HFG_MEL_BTC;
   if (o && o->mel_layout != HFG_MEL_BCT && o->mel_layout != HFG_MEL_BTC)
@@ -1097,9 +1252,16 @@ int forward_impl(hfg_handle* h, const float* mel, int64_t B, int64_t T, const hf
   if (sh.item_elems > ((int64_t)1 << 30))
     return fail(HFG_EINVAL, "per-item activation of %lld elements exceeds 2^30 (T too long)",
                 (long long)sh.item_elems);
-  if (ws_len < ws_part_bytes(h, B, T)) return fail(HFG_EINVAL, "workspace too small");
-  float* buf[4];
-  for (int i = 0; i < 4; ++i) buf[i] = reinterpret_cast<float*>(ws) + (size_t)i * sh.buf_elems;
+  if (ws_len < ws_part_bytes(h, B, T, conc_ok)) return fail(HFG_EINVAL, "workspace too small");
+  const int nb = n_bufs(h, B, T, conc_ok);
+  float* buf[4 + 3 * HFG_MAX_RES];
+  for (int i = 0; i < nb; ++i) buf[i] = reinterpret_cast<float*>(ws) + (size_t)i * sh.buf_elems;
+  RbConc conc{};
+  for (int j = 0; nb > 4 && j < h->cfg.n_res; ++j) {
+    conc.R[j] = buf[4 + 3 * j];
+    conc.Tb[j] = buf[5 + 3 * j];
+    conc.O[j] = buf[6 + 3 * j];
+  }
   float* X = buf[0];    // upsampled stage input
   float* R = buf[1];    // running ResBlock state (also conv_pre output)
   float* Tb = buf[2];   // conv1 output
@@ -1110,7 +1272,8 @@ int forward_impl(hfg_handle* h, const float* mel, int64_t B, int64_t T, const hf
   // ragged batch: per-stage valid lengths, computed on the device from lengths[B]
   const int32_t* lt = nullptr;  // lt + s*B = lengths after s upsample stages
   if (user_lens) {
-    int32_t* table = reinterpret_cast<int32_t*>(buf[3] + sh.buf_elems);
+    int32_t* table = reinterpret_cast<int32_t*>(reinterpret_cast<float*>(ws) +
+                                                (size_t)nb * sh.buf_elems);
     hfg::StageLenParams sp{};
     sp.n_up = c.n_up;
     sp.T = (int)T;
@@ -1143,7 +1306,8 @@ int forward_impl(hfg_handle* h, const float* mel, int64_t B, int64_t T, const hf
     if (rc) return rc;
     if ((rc = tap(1 + 2 * i, X, B * st.C * L))) return rc;
     // MRF (models/hifigan.py:116-131) of ResBlocks (:72-86)
-    rc = run_mrf(h, ln, st, X, B, L, R, Tb, MRF, lens_at(i + 1), -1);
+    rc = run_mrf(h, ln, st, X, B, L, R, Tb, MRF, lens_at(i + 1), -1,
+                 nb > 4 && stage_conc(h, st, B, L) ? &conc : nullptr);
     if (rc) return rc;
     if ((rc = tap(2 + 2 * i, MRF, B * st.C * L))) return rc;
     cur = MRF;
@@ -1171,7 +1335,7 @@ int forward_split(hfg_handle* h, const float* mel, int64_t B, int64_t T,
                   hipStream_t stream) {
   ++h->fwd_count;
   if (!split_batch(h, B, T))
-    return forward_impl(h, mel, B, T, o, wav, out_len, ws, ws_len, stream);
+    return forward_impl(h, mel, B, T, o, wav, out_len, ws, ws_len, stream, 0, nullptr, true);
   if (B <= 0 || T <= 0) return fail(HFG_EINVAL, "B and T must be > 0");
   if (ws_len < ws_bytes_for(h, B, T)) return fail(HFG_EINVAL, "workspace too small");
   if (!h->aux) {
@@ -1220,11 +1384,14 @@ int create_impl(const hfg_config* cfg, bool mrf_only, int device, hfg_handle** o
   if (const char* dbg = getenv("HFG_DEBUG_FLAGS")) h->dbg_flags = atoi(dbg);
   if (const char* bt = getenv("HFG_BF16X3_BIGTILE")) {
     const int v = atoi(bt);
-    if (v == 0 || v == 3 || v == hfg::kWsTile) h->big_tile = v;
+    if (v == 0 || v == 3) h->big_tile = v;
+    if (v == 4) h->big_tile = hfg::kWsTile;
   }
   if (const char* fe = getenv("HFG_FUSED_RB")) h->use_fused_rb = atoi(fe) != 0;
   if (const char* me = getenv("HFG_MFMA16")) h->mfma16 = atoi(me) != 0;
   if (const char* te = getenv("HFG_THIN")) h->thin = atoi(te) != 0;
+  if (const char* st = getenv("HFG_SMALL_TILE")) h->small_tile = atoi(st);
+  if (const char* rc = getenv("HFG_RB_CONC")) h->rb_conc = atoi(rc);
   if (const char* ce = getenv("HFG_C16")) h->c16 = atoi(ce) != 0;
   if (const char* se = getenv("HFG_SPLIT")) h->split = atoi(se);
   if (const char* rn = getenv("HFG_RB64_NARROW")) h->rb64_narrow = atoi(rn) != 0;
@@ -1290,6 +1457,13 @@ void hfg_destroy(hfg_handle* h) {
       if (h->fork_ev) (void)hipEventDestroy(h->fork_ev);
       if (h->join_ev) (void)hipEventDestroy(h->join_ev);
       if (h->aux) (void)hipStreamDestroy(h->aux);
+      for (int part = 0; part < 2; ++part) {
+        if (h->rb_fork[part]) (void)hipEventDestroy(h->rb_fork[part]);
+        for (int j = 0; j < HFG_MAX_RES; ++j) {
+          if (h->rb_join[part][j]) (void)hipEventDestroy(h->rb_join[part][j]);
+          if (h->rb_aux[part][j]) (void)hipStreamDestroy(h->rb_aux[part][j]);
+        }
+      }
     }
   }
   delete h;
@@ -1704,7 +1878,7 @@ int hfg_forward_taps(hfg_handle* h, const float* mel, int64_t B, int64_t T, floa
   }
   ++h->fwd_count;
   return forward_impl(h, mel, B, T, nullptr, wav, out_len, workspace, workspace_bytes,
-                      reinterpret_cast<hipStream_t>(stream), 0, taps);
+                      reinterpret_cast<hipStream_t>(stream), 0, taps, !split_batch(h, B, T));
 }
 
 }  // extern "C"

@@ -95,14 +95,23 @@ struct Bf16x3Cfg {
   constexpr int NTILE() const { return 32 * WN * WAVES_N; }
   constexpr int threads() const { return 64 * WAVES_M * WAVES_N; }
 };
-constexpr int kBf16x3Tiles_n = 4;
+constexpr int kBf16x3Tiles_n = 5;
 // 0: 128x256, 2x4 waves of 64x64, 4 taps/chunk, 3-deep weight ring (1 block/CU)
 // 1: 64x256, 1x4 waves of 64x64, 2 taps/chunk (2 blocks/CU)
 // 2: 32x256, 1x4 waves of 32x64, 4 taps/chunk (2 blocks/CU)
 // 3: 128x256, 2x2 waves of 64x128, 2 taps/chunk (2 blocks/CU: one block's epilogue
 //    overlaps the other's main loop)
+// 4: 64x64, 2x1 waves of 32x64, 4 taps/chunk: the small-grid tile.  A launch whose
+//    tile-3 grid would leave most CUs idle (small batches, short utterances) runs on it
+//    instead; every output element sees the same MFMA sequence (channel groups x taps in
+//    order, lo*hi, hi*lo, hi*hi) on either tile, so the choice is bitwise invisible.
 constexpr Bf16x3Cfg kBf16x3Tiles[kBf16x3Tiles_n] = {
-    {2, 4, 2, 2, 4, 3}, {1, 4, 2, 2, 2, 2}, {1, 4, 1, 2, 4, 2}, {2, 2, 2, 4, 2, 2}};
+    {2, 4, 2, 2, 4, 3}, {1, 4, 2, 2, 2, 2}, {1, 4, 1, 2, 4, 2}, {2, 2, 2, 4, 2, 2},
+    {2, 1, 1, 2, 4, 2}};
+constexpr int kBf16x3SmallTile = 4;
+// a layer launch runs on the small tile when its tile-3 grid has fewer blocks than this
+// (tile 3 fits 2 blocks per CU: 512 slots on 256 CUs)
+constexpr int kSmallGridBlocks = 256;
 constexpr int kBf16x3Ck = 16;  // channels per chunk (one MFMA k-step per tap)
 // largest (KT-1)*dil window halo of the bf16x3 layer kernel (sizes its staging
 // registers: 3 tasks per thread for the 256-column tiles); wider layers run on the fp32 path
@@ -122,7 +131,7 @@ hipError_t launch_conv_bf16x3(int tile, int kt, bool ups, const ConvParams& p, i
 // 128 x 256 block tile, 4 consumer waves (64 x 128 each) + 4 producer waves; weights
 // streamed from global memory, packed [m_tile][wave_m][group][tap][wm][plane][lane][8].
 // Selected with tile id kWsTile in the host layer table.
-constexpr int kWsTile = 4;
+constexpr int kWsTile = 8;   // tile id (HFG_BF16X3_BIGTILE=4 selects it)
 constexpr int kWsWaves = 8;
 constexpr int kWsMT = 128;
 constexpr int kWsNT = 256;
@@ -135,7 +144,7 @@ hipError_t launch_conv_ws_bf16x3(int kt, bool ups, const ConvParams& p, int n_ti
 // 128 x 256 block tile, 4 waves of 64 x 128; K walked as (channel group, tap) entries two
 // per k-step; A packed per k-step [m_tile][step][plane][wave_m][row tile][lane][8].
 // Needs an even channel-group count and (KT-1)*dil <= kC16MaxHalo.
-constexpr int kC16Tile = 5;
+constexpr int kC16Tile = 9;  // tile id
 constexpr int kC16MT = 128;
 constexpr int kC16NT = 256;
 constexpr int kC16MaxHalo = 128;
@@ -232,6 +241,17 @@ struct ChecksumArgs {
   int count, base;
 };
 hipError_t launch_checksum(const ChecksumArgs& a, uint32_t* out, hipStream_t stream);
+
+// y = (o_0 + o_1 + ... (in order)) / div over [B][C][L], columns < len[b] (len null = L)
+constexpr int kMrfCombineMax = 8;
+struct MrfCombineArgs {
+  const float* o[kMrfCombineMax];
+  int n, C, L;
+  const int32_t* len;
+  float* y;
+  float div;
+};
+hipError_t launch_mrf_combine(const MrfCombineArgs& a, int batch, hipStream_t stream);
 
 // Per-stage valid lengths of a ragged batch: out[s*B + b] = length after s
 // upsample stages of an utterance with lens[b] frames (clamped to [0, T]).
