@@ -39,7 +39,7 @@ def _gen(pkg, cfg, sd, dev, precision, env):
     return gen
 
 
-@pytest.mark.parametrize("preset,B,T", [("v1", 1, 96), ("v1", 3, 40), ("v2star", 2, 64)])
+@pytest.mark.parametrize("preset,B,T", [("v1", 1, 96), ("v1", 3, 40), ("v2star", 2, 64), ("v1", 2, 300)])
 def test_small_tile_is_bitwise_invisible(pkg, dev, preset, B, T):
     from oracle import config as C, hifigan_torch as H
     cfg = C.PRESETS[preset]

@@ -69,9 +69,23 @@ conv1d_bf16x3(const ConvParams p) {
   const int wave = tid >> 6;
   const int wave_m = wave % WAVES_M;
   const int wave_n = wave / WAVES_M;
-  const int n0 = blockIdx.x * NTILE;
-  const int mt = blockIdx.y;
-  const int b = blockIdx.z;
+  // block -> (column tile, m-tile, item).  Upsamplers: the m-tiles of one input window
+  // (16 for ups.0) read the same x rows, so they are swizzled onto one XCD's L2 (blocks b
+  // and b + 8 share an XCD under the round-robin placement; speed only, any placement is
+  // correct): linear id -> (id % 8) * (total / 8) + id / 8, then m-tile fastest.
+  int tx = blockIdx.x, mt = blockIdx.y, b = blockIdx.z;
+  if (UPS && p.ups_swz) {
+    const int nx = gridDim.x, ny = gridDim.y;
+    const int total = nx * ny * gridDim.z;
+    int id = blockIdx.x + nx * (blockIdx.y + ny * blockIdx.z);
+    const int q = total >> 3;
+    if (id < (q << 3)) id = (id & 7) * q + (id >> 3);
+    mt = id % ny;
+    id /= ny;
+    tx = id % nx;
+    b = id / nx;
+  }
+  const int n0 = p.n_base + tx * NTILE;
   const int half = lane >> 5;
   const int col = lane & 31;
   const float* __restrict__ xb = p.x + (int64_t)b * p.x_bs;

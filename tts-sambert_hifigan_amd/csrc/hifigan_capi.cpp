@@ -133,6 +133,7 @@ struct hfg_handle {
   int rb_waves_n32 = 4;      // window of the C = 32 ResBlock kernel: 128 * this columns
                              // (HFG_RB_WN32: 4 or 8)
   bool mfma16 = true;        // 16x16x32-shape ResBlock kernel for C = 32 (HFG_MFMA16=0: off)
+  int ups_swizzle = 1;       // XCD swizzle of the upsampler blocks (HFG_UPS_SWIZZLE=0: off)
   int small_tile = -1;       // small-grid tile: -1 auto (grid < kSmallGridBlocks), 0 never,
                              // 1 always (HFG_SMALL_TILE)
   bool thin = true;          // whole-MRF VALU kernel for C <= 16 stages (HFG_THIN=0: layer
@@ -1042,6 +1043,7 @@ int run_ups(hfg_handle* h, Launcher& ln, const Layer& L, const float* x, int64_t
   p.act_out = 0;
   p.ups_s = L.s;
   p.ups_p = L.p;
+  p.ups_swz = h->ups_swizzle;
   p.L_out = (int)Lout;
   p.n_chunks = L.n_chunks;
   p.dbg = h->dbg_flags;
@@ -1392,6 +1394,7 @@ int create_impl(const hfg_config* cfg, bool mrf_only, int device, hfg_handle** o
   if (const char* te = getenv("HFG_THIN")) h->thin = atoi(te) != 0;
   if (const char* st = getenv("HFG_SMALL_TILE")) h->small_tile = atoi(st);
   if (const char* rc = getenv("HFG_RB_CONC")) h->rb_conc = atoi(rc);
+  if (const char* us = getenv("HFG_UPS_SWIZZLE")) h->ups_swizzle = atoi(us);
   if (const char* ce = getenv("HFG_C16")) h->c16 = atoi(ce) != 0;
   if (const char* se = getenv("HFG_SPLIT")) h->split = atoi(se);
   if (const char* rn = getenv("HFG_RB64_NARROW")) h->rb64_narrow = atoi(rn) != 0;

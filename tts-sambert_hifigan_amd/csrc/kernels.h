@@ -35,7 +35,9 @@ struct ConvParams {
   int mrf_mode;      // bit0: add existing mrf value, bit1: divide by mrf_div
   float mrf_div;
   int ups_s, ups_p, L_out;  // UPS store mapping
+  int ups_swz;              // UPS: XCD swizzle of the block order (bf16x3 kernel)
   int n_chunks;      // ceil(C_in / CK)
+  int n_base;        // first GEMM column of this launch (bf16x3 kernel; 0 elsewhere)
   int dbg;           // ablation flags (HFG_DEBUG_FLAGS; 0 in production; wrong results when
                      // set), bf16x3 kernel: bit0 skip input restaging after the first
                      // chunk, bit2 no per-chunk barrier, bit3 no epilogue
