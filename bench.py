@@ -280,6 +280,23 @@ def extra_configs(pkg, S, dev, precision, steps=5):
                                            "frames": lens[:8] + ["..."],
                                            "note": "vocoder half of config 5; the SAM-BERT "
                                                    "acoustic model is CPU reference code (out of scope)"}
+        # the mel row: log-mel of the C2 workload's audio, and the
+        # 16 kHz -> 22.05 kHz resampler on 8 one-second utterances
+        melmod = importlib.import_module(ge.PKG_NAME + ".mel")
+        ext = melmod.MelSpectrogram(device=dev)
+        audio = torch.randn(8, 262144, generator=g).clamp(-1, 1).to(dev)
+        for _ in range(2):
+            ext(audio)
+        t = timed(lambda: ext(audio), 20)
+        out["mel_8x262144"] = {"ms": t * 1e3, "frames_per_s": 8 * (262144 // 256 + 1) / t,
+                               "audio_samples_per_s": 8 * 262144 / t,
+                               "note": "hfg_mel_forward: windowed DFT on the fp32 MFMA + mel + log10"}
+        rs = melmod.Resample(16000, 22050, device=dev)
+        a16 = torch.randn(8, 16000, generator=g).clamp(-1, 1).to(dev)
+        for _ in range(2):
+            rs(a16)
+        t = timed(lambda: rs(a16), 20)
+        out["resample_16k_to_22k_8x1s"] = {"ms": t * 1e3, "out_samples_per_s": 8 * 22050 / t}
     return out
 
 

@@ -230,7 +230,10 @@ typedef struct hfg_mel_config {
     int32_t mel_scale;     /* 0 = slaney, 1 = htk            */
     int32_t norm;          /* 0 = none, 1 = slaney           */
     float log_eps;         /* 1e-10 (audio_processing.py:123) */
-    int32_t log_base;      /* 10 = log10, 0 = natural log    */
+    int32_t log_base;      /* 10 = log10, 0 = natural log,   */
+                           /* 1 = log(x) / log(log_base_value)*/
+                           /* (audio_processing.py:125-133)   */
+    float log_base_value;  /* the custom base (log_base == 1) */
 } hfg_mel_config;
 
 const char* hfg_mel_last_error(void);
@@ -242,6 +245,28 @@ int64_t hfg_mel_frames(const hfg_mel_handle* h, int64_t n_samples);
 size_t hfg_mel_workspace_bytes(const hfg_mel_handle* h, int64_t B, int64_t n_samples);
 int hfg_mel_forward(hfg_mel_handle* h, const float* wav, int64_t B, int64_t n_samples,
                     float* mel, void* workspace, size_t workspace_bytes, void* stream);
+
+/* ---------------------------------------------------------------------------
+ * On-device resampling ← extract_mel's torchaudio.transforms.Resample(orig, new)
+ * (data/audio_processing.py:81-88; torchaudio defaults: sinc_interp_hann,
+ * lowpass_filter_width 6, rolloff 0.99).  The polyphase sinc kernel
+ * [new/g][2*width + orig/g] (g = gcd) is built on the host in float64 and
+ * stored fp32; y[b][n*new/g + j] = sum_k x_pad[b][n*orig/g + k] * kernel[j][k]
+ * with x zero-padded by width on the left, width + orig/g on the right;
+ * out_len = ceil(n * new / orig).  orig == new copies.
+ * ------------------------------------------------------------------------- */
+typedef struct hfg_resample_handle hfg_resample_handle;
+/* host side: the kernel table (NULL kernel = sizes only) */
+int hfg_resample_kernel(int32_t orig_freq, int32_t new_freq, int32_t lowpass_filter_width,
+                        float rolloff, float* kernel, int32_t* width, int32_t* n_phases,
+                        int32_t* kernel_len);
+int hfg_resample_create(int32_t orig_freq, int32_t new_freq, int32_t lowpass_filter_width,
+                        float rolloff, int device, hfg_resample_handle** out);
+void hfg_resample_destroy(hfg_resample_handle* h);
+int64_t hfg_resample_out_len(const hfg_resample_handle* h, int64_t n_samples);
+/* y[B][out_len] = Resample(x[B][n_samples]), async on stream */
+int hfg_resample_forward(hfg_resample_handle* h, const float* x, int64_t B, int64_t n_samples,
+                         float* y, void* stream);
 
 #ifdef __cplusplus
 }

@@ -2,8 +2,12 @@
 restatement (oracle/mel_torch.py).  PARITY UNPINNED: torchaudio, which the
 reference calls, is absent from this image, so the oracle is a restatement of
 its published algorithm (same torch.stft call, same float32 filterbank code).
-Tolerance: |log10 mel - oracle| <= 2e-3 where the oracle mel >= 1e-6 x its max
-(fp32 DFT by direct summation vs pocketfft), and <= 5e-2 everywhere else."""
+Tolerance (fp32 DFT by direct summation vs pocketfft): |log10 mel - oracle| <= 1e-4
+where the oracle mel >= 1e-2 x its max (the bands that carry the signal: a relative
+power error of ~2e-4; measured <= 3e-5), <= 5e-4 where it is >= 1e-6 x its max
+(measured <= 7e-5), and <= 2e-2 everywhere else (measured <= 6.2e-3) (bins ~60 dB below the peak, where the fp32 summation's absolute error of ~1e-7 of
+the peak power dominates).  The resampler (torchaudio Resample restated in
+oracle/resample_np.py, float64) is checked at 2e-6 x max|x|."""
 import numpy as np
 import pytest
 import torch
@@ -28,10 +32,14 @@ def _signals(n):
 
 
 def _check(got, ref):
+    strong = ref >= np.log10(1e-2) + ref.max()
     big = ref >= np.log10(1e-6) + ref.max()
     err = (got - ref).abs()
-    assert err[big].max().item() <= 2e-3, err[big].max().item()
-    assert err.max().item() <= 5e-2, err.max().item()
+    print(f"\nlog-mel error: strong {err[strong].max().item():.2e}, "
+          f">=1e-6 {err[big].max().item():.2e}, all {err.max().item():.2e}")
+    assert err[strong].max().item() <= 1e-4, err[strong].max().item()
+    assert err[big].max().item() <= 5e-4, err[big].max().item()
+    assert err.max().item() <= 2e-2, err.max().item()
 
 
 @pytest.mark.parametrize("n", [22050 + 77, 513, 4096])
@@ -60,8 +68,68 @@ def test_extract_mel_contract(pkg, dev):
     assert mel.dim() == 2 and mel.size(0) == 80 and mel.shape[1] == 30000 // 256 + 1
     assert mel.max() <= 10
     _check(mel.cpu(), M.log_mel(stereo.mean(0)))
-    with pytest.raises(NotImplementedError):
-        melmod.extract_mel(stereo.to(dev), sample_rate=16000, config=cfg)
+
+
+@pytest.mark.parametrize("orig,new", [(16000, 22050), (44100, 22050), (48000, 22050),
+                                      (22050, 16000)])
+def test_resample_vs_restatement(pkg, dev, orig, new):
+    """torchaudio.transforms.Resample (audio_processing.py:84-88) on the GPU vs the float64
+    restatement of its algorithm (oracle/resample_np.py).  PARITY UNPINNED."""
+    import importlib
+    melmod = importlib.import_module("tts_sambert_hifigan_amd.mel")
+    from oracle import resample_np as R
+    g = torch.Generator().manual_seed(orig)
+    x = (0.4 * torch.randn(3, 7777, generator=g)).clamp(-1, 1)
+    rs = melmod.Resample(orig, new, device=dev)
+    y = rs(x.to(dev)).cpu().numpy()
+    ref = R.resample(x.numpy(), orig, new)
+    assert y.shape == ref.shape == (3, -(-7777 * new // orig))
+    err = np.abs(y - ref).max()
+    print(f"\nresample {orig}->{new}: max err {err:.2e}")
+    assert err <= 2e-6 * np.abs(x.numpy()).max()
+    k, width = rs.kernel()
+    rk, rw = R.sinc_kernel(orig, new)
+    assert width == rw and np.abs(k.numpy() - rk).max() <= 1e-7
+
+
+def test_extract_mel_resamples_and_prints(pkg, dev, capsys):
+    """extract_mel(sample_rate=16000) resamples to the config's 22050 Hz (per channel,
+    then the mono mean, as audio_processing.py:81-96 orders it) and prints the
+    reference's debug.print_shapes lines."""
+    import importlib
+    melmod = importlib.import_module("tts_sambert_hifigan_amd.mel")
+    from oracle import mel_torch as M, resample_np as R
+    cfg = {"audio": {"sample_rate": 22050, "n_fft": 1024, "hop_length": 256, "win_length": 1024,
+                     "n_mels": 80, "fmin": 0, "fmax": 8000, "log_base": 10.0},
+           "debug": {"print_shapes": True}}
+    stereo = _signals(16000)
+    mel = melmod.extract_mel(stereo.to(dev), sample_rate=16000, config=cfg)
+    out = capsys.readouterr().out
+    for line in ("[extract_mel] Input waveform shape: torch.Size([2, 16000])",
+                 "[extract_mel] Resampling from 16000Hz to 22050Hz",
+                 "[extract_mel] Resampled waveform shape: torch.Size([2, 22050])",
+                 "[extract_mel] Converted to mono, shape: torch.Size([1, 22050])",
+                 "[extract_mel] Mel spectrogram shape (before log): torch.Size([80, 87])",
+                 "[extract_mel] Log-mel spectrogram shape: torch.Size([80, 87])",
+                 "[extract_mel] Log-mel range: ["):
+        assert line in out, (line, out)
+    ref_wav = torch.from_numpy(R.resample(stereo.numpy(), 16000, 22050)).mean(0)
+    assert mel.shape == (80, 22050 // 256 + 1)
+    _check(mel.cpu(), M.log_mel(ref_wav))
+
+
+@pytest.mark.parametrize("base", [2.0, "e", 10.0])
+def test_log_base(pkg, dev, base):
+    """audio_processing.py:125-133: log10, natural log, or log(x) / log(base)."""
+    import importlib
+    import math
+    melmod = importlib.import_module("tts_sambert_hifigan_amd.mel")
+    from oracle import mel_torch as M
+    wav = _signals(8000)
+    got = melmod.MelSpectrogram(log_base=base, device=dev)(wav.to(dev)).cpu()
+    ref10 = M.log_mel(wav)
+    scale = {2.0: math.log(10) / math.log(2), "e": math.log(10), 10.0: 1.0}[base]
+    _check(got / scale, ref10)
 
 
 def test_mel_feeds_vocoder(pkg, dev):

@@ -133,7 +133,7 @@ class HfgMelConfig(ctypes.Structure):
     _fields_ = [("sample_rate", c_int32), ("n_fft", c_int32), ("hop_length", c_int32),
                 ("win_length", c_int32), ("n_mels", c_int32), ("f_min", c_float),
                 ("f_max", c_float), ("mel_scale", c_int32), ("norm", c_int32),
-                ("log_eps", c_float), ("log_base", c_int32)]
+                ("log_eps", c_float), ("log_base", c_int32), ("log_base_value", c_float)]
 
 
 _lib = None
@@ -180,6 +180,12 @@ SIGNATURES = {
     "hfg_mel_workspace_bytes": (c_size_t, [c_void_p, c_int64, c_int64]),
     "hfg_mel_forward": (c_int, [c_void_p, c_void_p, c_int64, c_int64, c_void_p, c_void_p,
                                 c_size_t, c_void_p]),
+    "hfg_resample_kernel": (c_int, [c_int32, c_int32, c_int32, c_float, POINTER(c_float),
+                                    POINTER(c_int32), POINTER(c_int32), POINTER(c_int32)]),
+    "hfg_resample_create": (c_int, [c_int32, c_int32, c_int32, c_float, c_int, POINTER(c_void_p)]),
+    "hfg_resample_destroy": (None, [c_void_p]),
+    "hfg_resample_out_len": (c_int64, [c_void_p, c_int64]),
+    "hfg_resample_forward": (c_int, [c_void_p, c_void_p, c_int64, c_int64, c_void_p, c_void_p]),
 }
 
 

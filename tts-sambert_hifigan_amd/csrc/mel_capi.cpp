@@ -8,6 +8,7 @@
 // periodic Hann) and the log at :123-133.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -92,6 +93,10 @@ int hfg_mel_create(const hfg_mel_config* c, int device, hfg_mel_handle** out) {
     return mfail(HFG_EINVAL, "invalid mel configuration");
   if (c->mel_scale != 0 && c->mel_scale != 1) return mfail(HFG_EINVAL, "mel_scale 0|1");
   if (c->norm != 0 && c->norm != 1) return mfail(HFG_EINVAL, "norm 0|1");
+  if (c->log_base != 10 && c->log_base != 0 && c->log_base != 1)
+    return mfail(HFG_EINVAL, "log_base: 10 (log10), 0 (ln) or 1 (custom base)");
+  if (c->log_base == 1 && !(c->log_base_value > 0.f && c->log_base_value != 1.f))
+    return mfail(HFG_EINVAL, "custom log base must be > 0 and != 1");
   if ((size_t)(31 * c->hop_length + c->n_fft) * 4 * 33 / 32 > 64 * 1024)
     return mfail(HFG_EINVAL, "n_fft / hop too large for the LDS frame tile");
   auto* h = new (std::nothrow) hfg_mel_handle();
@@ -184,9 +189,143 @@ int hfg_mel_forward(hfg_mel_handle* h, const float* wav, int64_t B, int64_t n_sa
                                         s);
   if (e == hipSuccess)
     e = hfg::launch_mel_log(power, B, n_frames, h->n_bins, h->fb, h->cfg.n_mels, h->cfg.log_eps,
-                            h->cfg.log_base == 10 ? 1 : 0, mel, s);
+                            h->cfg.log_base == 10 ? 1 : (h->cfg.log_base == 0 ? 0 : 2),
+                            // torch.log(torch.tensor(log_base)): a float32 log of the base
+                            std::log(h->cfg.log_base_value), mel, s);
   if (prev >= 0 && prev != h->device) (void)hipSetDevice(prev);
   if (e != hipSuccess) return mfail(HFG_EIO, "mel launch: %s", hipGetErrorString(e));
+  return HFG_OK;
+}
+
+}  // extern "C"
+
+// ---- resampling (torchaudio.transforms.Resample, audio_processing.py:81-88) ----------
+struct hfg_resample_handle {
+  int orig, new_, g;          // reduced rates orig / g, new / g
+  int width, klen;
+  int device;
+  float* kern = nullptr;      // [new][klen] on the device
+};
+
+namespace {
+long long gcd_ll(long long a, long long b) {
+  while (b) {
+    const long long t = a % b;
+    a = b;
+    b = t;
+  }
+  return a;
+}
+}  // namespace
+
+extern "C" {
+
+// torchaudio.functional._get_sinc_resample_kernel(orig, new, gcd, lowpass_filter_width,
+// rolloff, "sinc_interp_hann", dtype=None): float64 arithmetic (the phase offsets j/new
+// are a float32 division of an integer tensor, as there), stored float32.
+int hfg_resample_kernel(int32_t orig_freq, int32_t new_freq, int32_t lpw, float rolloff,
+                        float* kernel, int32_t* width_out, int32_t* n_phases, int32_t* klen_out) {
+  if (orig_freq <= 0 || new_freq <= 0 || lpw <= 0 || !(rolloff > 0.f && rolloff <= 1.f))
+    return mfail(HFG_EINVAL, "resample: rates and lowpass_filter_width must be > 0, "
+                 "0 < rolloff <= 1");
+  const long long g = gcd_ll(orig_freq, new_freq);
+  const long long orig = orig_freq / g, nw = new_freq / g;
+  const double base = (double)std::min(orig, nw) * (double)rolloff;
+  const int width = (int)std::ceil((double)lpw * (double)orig / base);
+  const int klen = 2 * width + (int)orig;
+  if (width_out) *width_out = width;
+  if (n_phases) *n_phases = (int32_t)nw;
+  if (klen_out) *klen_out = klen;
+  if (!kernel) return HFG_OK;
+  const double pi = 3.14159265358979323846;
+  for (long long j = 0; j < nw; ++j) {
+    const double off = (double)((float)(-j) / (float)nw);
+    for (int k = 0; k < klen; ++k) {
+      double t = (off + (double)(k - width) / (double)orig) * base;
+      t = std::min((double)lpw, std::max(-(double)lpw, t));
+      const double c = std::cos(t * pi / lpw / 2);
+      const double window = c * c;
+      t *= pi;
+      const double v = (t == 0.0 ? 1.0 : std::sin(t) / t) * (window * (base / (double)orig));
+      kernel[j * klen + k] = (float)v;
+    }
+  }
+  return HFG_OK;
+}
+
+int hfg_resample_create(int32_t orig_freq, int32_t new_freq, int32_t lpw, float rolloff,
+                        int device, hfg_resample_handle** out) {
+  if (!out) return mfail(HFG_EINVAL, "out is NULL");
+  *out = nullptr;
+  int32_t width = 0, np = 0, klen = 0;
+  int rc = hfg_resample_kernel(orig_freq, new_freq, lpw, rolloff, nullptr, &width, &np, &klen);
+  if (rc) return rc;
+  const long long g = gcd_ll(orig_freq, new_freq);
+  if ((long long)np * klen > (1LL << 24))
+    return mfail(HFG_EINVAL, "resample kernel [%d][%d] too large (rates %d -> %d)", np, klen,
+                 orig_freq, new_freq);
+  if ((size_t)((255 / np + 1) * (orig_freq / g) + klen) * sizeof(float) > 64 * 1024)
+    return mfail(HFG_EINVAL, "resample ratio %d -> %d too large for the LDS input span",
+                 orig_freq, new_freq);
+  auto* h = new (std::nothrow) hfg_resample_handle();
+  if (!h) return mfail(HFG_ENOMEM, "host alloc");
+  h->orig = (int)(orig_freq / g);
+  h->new_ = np;
+  h->g = (int)g;
+  h->width = width;
+  h->klen = klen;
+  h->device = device;
+  if (device >= 0) {
+    std::vector<float> k((size_t)np * klen);
+    hfg_resample_kernel(orig_freq, new_freq, lpw, rolloff, k.data(), nullptr, nullptr, nullptr);
+    int prev = -1;
+    (void)hipGetDevice(&prev);
+    if (hipSetDevice(device) != hipSuccess) {
+      delete h;
+      return mfail(HFG_ENODEV, "hipSetDevice(%d)", device);
+    }
+    if (hipMalloc(&h->kern, k.size() * sizeof(float)) != hipSuccess ||
+        hipMemcpy(h->kern, k.data(), k.size() * sizeof(float), hipMemcpyHostToDevice) !=
+            hipSuccess) {
+      hfg_resample_destroy(h);
+      return mfail(HFG_ENOMEM, "resample kernel upload");
+    }
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+  *out = h;
+  return HFG_OK;
+}
+
+void hfg_resample_destroy(hfg_resample_handle* h) {
+  if (!h) return;
+  if (h->kern) (void)hipFree(h->kern);
+  delete h;
+}
+
+int64_t hfg_resample_out_len(const hfg_resample_handle* h, int64_t n) {
+  if (!h || n < 0) return -1;
+  // torch.ceil(torch.as_tensor(new * length / orig)) on the reduced rates (a float64 quotient)
+  return (int64_t)std::ceil((double)h->new_ * (double)n / (double)h->orig);
+}
+
+int hfg_resample_forward(hfg_resample_handle* h, const float* x, int64_t B, int64_t n, float* y,
+                         void* stream) {
+  if (!h || !x || !y) return mfail(HFG_EINVAL, "NULL argument");
+  if (h->device < 0) return mfail(HFG_EINVAL, "host-only resample handle");
+  if (B <= 0 || n <= 0) return mfail(HFG_EINVAL, "B and n_samples must be > 0");
+  const int64_t n_out = hfg_resample_out_len(h, n);
+  int prev = -1;
+  (void)hipGetDevice(&prev);
+  if (prev != h->device && hipSetDevice(h->device) != hipSuccess)
+    return mfail(HFG_ENODEV, "hipSetDevice(%d)", h->device);
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  hipError_t e;
+  if (h->orig == h->new_)
+    e = hipMemcpyAsync(y, x, sizeof(float) * (size_t)(B * n), hipMemcpyDeviceToDevice, s);
+  else
+    e = hfg::launch_resample(x, B, n, n_out, h->kern, h->new_, h->orig, h->klen, h->width, y, s);
+  if (prev >= 0 && prev != h->device) (void)hipSetDevice(prev);
+  if (e != hipSuccess) return mfail(HFG_EIO, "resample launch: %s", hipGetErrorString(e));
   return HFG_OK;
 }
 

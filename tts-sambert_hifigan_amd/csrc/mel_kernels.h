@@ -12,9 +12,16 @@ hipError_t launch_stft_power(const float* wav, int64_t B, int64_t N, int n_fft, 
                              int n_bins, int n_frames, const float* tcos, const float* tsin,
                              int bins_pad, float* power, hipStream_t stream);
 
-// mel[b][m][f] = log(sum_k fb[k][m] * power[b][f][k] + eps)  (log10 or ln)
+// mel[b][m][f] = log(sum_k fb[k][m] * power[b][f][k] + eps): log_mode 1 log10, 0 ln,
+// 2 ln(v) / ln_base (a custom base, audio_processing.py:131-133)
 hipError_t launch_mel_log(const float* power, int64_t B, int n_frames, int n_bins,
-                          const float* fb, int n_mels, float eps, int log10_out, float* mel,
-                          hipStream_t stream);
+                          const float* fb, int n_mels, float eps, int log_mode, float ln_base,
+                          float* mel, hipStream_t stream);
+
+// y[b][m] = sum_k x_pad[b][(m / n_phases) * stride + k] * kern[m % n_phases][k], m < n_out,
+// x_pad = x zero-padded by `width` on the left (torchaudio _apply_sinc_resample_kernel)
+hipError_t launch_resample(const float* x, int64_t B, int64_t n, int64_t n_out,
+                           const float* kern, int n_phases, int stride, int klen, int width,
+                           float* y, hipStream_t stream);
 
 }  // namespace hfg

@@ -81,7 +81,7 @@ stft_power_mfma(const float* __restrict__ wav, int64_t N, int n_fft, int hop, in
 // block: 16 frames of one utterance; power rows staged in LDS; thread = (frame, mel)
 __global__ void __launch_bounds__(256)
 mel_log(const float* __restrict__ power, int n_frames, int n_bins, const float* __restrict__ fb,
-        int n_mels, float eps, int log10_out, float* __restrict__ mel) {
+        int n_mels, float eps, int log_mode, float ln_base, float* __restrict__ mel) {
   extern __shared__ __attribute__((aligned(16))) float pw[];
   constexpr int FT = 16;
   const int b = blockIdx.y;
@@ -96,7 +96,8 @@ mel_log(const float* __restrict__ power, int n_frames, int n_bins, const float* 
     float acc = 0.f;
     for (int k = 0; k < n_bins; ++k) acc = fmaf(fb[(int64_t)k * n_mels + m], p[k], acc);
     const float v = acc + eps;
-    mel[((int64_t)b * n_mels + m) * n_frames + f0 + f] = log10_out ? log10f(v) : logf(v);
+    mel[((int64_t)b * n_mels + m) * n_frames + f0 + f] =
+        log_mode == 1 ? log10f(v) : (log_mode == 0 ? logf(v) : logf(v) / ln_base);
   }
 }
 
@@ -113,13 +114,58 @@ hipError_t launch_stft_power(const float* wav, int64_t B, int64_t N, int n_fft, 
 }
 
 hipError_t launch_mel_log(const float* power, int64_t B, int n_frames, int n_bins,
-                          const float* fb, int n_mels, float eps, int log10_out, float* mel,
-                          hipStream_t stream) {
+                          const float* fb, int n_mels, float eps, int log_mode, float ln_base,
+                          float* mel, hipStream_t stream) {
   const size_t lds = sizeof(float) * (size_t)16 * n_bins;
   if (lds > 64 * 1024) return hipErrorInvalidValue;
   dim3 grid((n_frames + 15) / 16, (unsigned)B);
-  mel_log<<<grid, dim3(256), lds, stream>>>(power, n_frames, n_bins, fb, n_mels, eps, log10_out,
-                                            mel);
+  mel_log<<<grid, dim3(256), lds, stream>>>(power, n_frames, n_bins, fb, n_mels, eps, log_mode,
+                                            ln_base, mel);
+  return hipGetLastError();
+}
+
+// Polyphase sinc resampling (torchaudio _apply_sinc_resample_kernel: conv1d of the padded
+// signal with the [n_phases][klen] kernel at stride `stride`, phases interleaved).  A block
+// owns 256 consecutive outputs; the input span they read (<= 256/n_phases*stride + klen
+// samples) is staged in LDS once, zero outside [0, n), and every output is one dot product
+// of klen taps: an HBM-bound stream (reads ~stride/n_phases inputs per output).
+__global__ void __launch_bounds__(256)
+resample_sinc(const float* __restrict__ x, int64_t n, int64_t n_out,
+              const float* __restrict__ kern, int n_phases, int stride, int klen, int width,
+              float* __restrict__ y) {
+  extern __shared__ float xs[];
+  const int b = blockIdx.y;
+  const int64_t m0 = (int64_t)blockIdx.x * 256;
+  const int64_t q0 = m0 / n_phases;                     // first output frame of the block
+  const int64_t q1 = (min(m0 + 256, n_out) - 1) / n_phases;
+  const int64_t s0 = q0 * stride - width;               // first input sample read
+  const int span = (int)((q1 - q0) * stride + klen);
+  const float* xb = x + (int64_t)b * n;
+  for (int i = threadIdx.x; i < span; i += 256) {
+    const int64_t g = s0 + i;
+    xs[i] = (g >= 0 && g < n) ? xb[g] : 0.f;
+  }
+  __syncthreads();
+  const int64_t m = m0 + threadIdx.x;
+  if (m >= n_out) return;
+  const int64_t q = m / n_phases;
+  const int j = (int)(m - q * n_phases);
+  const float* kr = kern + (int64_t)j * klen;
+  const float* xr = xs + (q - q0) * stride;
+  float acc = 0.f;
+  for (int k = 0; k < klen; ++k) acc = fmaf(xr[k], kr[k], acc);
+  y[(int64_t)b * n_out + m] = acc;
+}
+
+hipError_t launch_resample(const float* x, int64_t B, int64_t n, int64_t n_out,
+                           const float* kern, int n_phases, int stride, int klen, int width,
+                           float* y, hipStream_t stream) {
+  const int64_t span = (int64_t)(255 / n_phases + 1) * stride + klen;
+  const size_t lds = sizeof(float) * (size_t)span;
+  if (lds > 64 * 1024) return hipErrorInvalidValue;
+  dim3 grid((unsigned)((n_out + 255) / 256), (unsigned)B);
+  resample_sinc<<<grid, dim3(256), lds, stream>>>(x, n, n_out, kern, n_phases, stride, klen,
+                                                  width, y);
   return hipGetLastError();
 }
 
