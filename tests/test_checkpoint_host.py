@@ -1,0 +1,92 @@
+"""Checkpoint layouts (tts-sambert_hifigan_amd/checkpoint.py) on the
+CPU: every supported layout loads into the drop-in Generator with the weights the
+reference would compute (weight norm folded by torch._weight_norm, bitwise)."""
+import importlib
+
+import pytest
+import torch
+import torch.nn as nn
+
+from oracle import config as C
+
+
+@pytest.fixture(scope="module")
+def ck(pkg):
+    return importlib.import_module("tts_sambert_hifigan_amd.checkpoint")
+
+
+def _ref_weights(cfg, seed):
+    return {k: torch.from_numpy(v) for k, v in C.make_state_dict(cfg, seed).items()}
+
+
+def _public_layout(sd, cfg):
+    """The public HiFi-GAN release layout: weight norm on every conv (conv_pre and
+    conv_post too), ResBlocks flat-indexed, inside {"generator": ...}."""
+    K = len(cfg.resblock_kernel_sizes)
+    out = {}
+    for k, v in sd.items():
+        parts = k.split(".")
+        if parts[0] == "mrfs":
+            k = f"resblocks.{int(parts[1]) * K + int(parts[3])}." + ".".join(parts[4:])
+        if k.endswith(".weight"):
+            mod = k[: -len(".weight")]
+            # g = ||v|| over every dim but 0, v = w: torch._weight_norm(v, g, 0) gives w back
+            g = torch.norm_except_dim(v, 2, 0)
+            out[mod + ".weight_g"] = g
+            out[mod + ".weight_v"] = v.clone()
+        else:
+            out[k] = v
+    return {"generator": out}
+
+
+@pytest.mark.parametrize("preset", ["v1", "v2star"])
+def test_public_release_layout(pkg, ck, preset):
+    cfg = C.PRESETS[preset]
+    sd = _ref_weights(cfg, 7)
+    gen = pkg.HiFiGANGenerator(**cfg.kwargs())
+    res = ck.load_generator_checkpoint(gen, _public_layout(sd, cfg))
+    assert not res.missing_keys and not res.unexpected_keys
+    got = gen.state_dict()
+    for k, v in sd.items():
+        ref = v
+        if k.endswith(".weight"):
+            ref = torch._weight_norm(v, torch.norm_except_dim(v, 2, 0), 0)
+        assert torch.equal(got[k], ref), k
+
+
+def test_wrapper_module_prefix_and_discriminators(pkg, ck, tmp_path):
+    cfg = C.V2STAR
+    sd = _ref_weights(cfg, 8)
+    wrapped = {"model": {"module.generator." + k: v for k, v in sd.items()}}
+    wrapped["model"]["module.msd.discriminators.0.convs.0.weight"] = torch.zeros(3)
+    wrapped["model"]["module.mpd.discriminators.0.convs.0.weight"] = torch.zeros(3)
+    path = tmp_path / "ck.pt"
+    torch.save(wrapped, path)
+    gen = pkg.HiFiGAN(**cfg.kwargs())
+    res = ck.load_generator_checkpoint(gen, str(path))
+    assert not res.missing_keys and not res.unexpected_keys
+    for k, v in sd.items():
+        assert torch.equal(gen.generator.state_dict()[k], v), k
+
+
+def test_weight_normed_target_keeps_g_v(pkg, ck):
+    """A Generator on which apply_weight_norm() was called keeps weight_g / weight_v of
+    ups and the ResBlock convs (the reference's weight-normed modules)."""
+    cfg = C.V2STAR
+    wn = {k: torch.from_numpy(v) for k, v in C.make_weight_norm_state_dict(cfg, 9).items()}
+    gen = pkg.HiFiGANGenerator(**cfg.kwargs())
+    gen.apply_weight_norm()
+    res = ck.load_generator_checkpoint(gen, {"generator": wn})
+    assert not res.missing_keys and not res.unexpected_keys
+    for k, v in wn.items():
+        assert torch.equal(gen.state_dict()[k], v), k
+
+
+def test_bad_layouts_rejected(pkg, ck):
+    gen = pkg.HiFiGANGenerator(**C.V2STAR.kwargs())
+    with pytest.raises(ValueError):
+        ck.load_generator_checkpoint(gen, {"optimizer": {"lr": 1}})
+    sd = _public_layout(_ref_weights(C.V2STAR, 3), C.V2STAR)["generator"]
+    sd["resblocks.99.convs1.0.bias"] = torch.zeros(8)
+    with pytest.raises(ValueError):
+        ck.load_generator_checkpoint(gen, sd)
