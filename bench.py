@@ -260,6 +260,16 @@ def extra_configs(pkg, S, dev, precision, steps=5):
                                  "samples_per_s_hipgraph": 65536 / replay,
                                  "rtf_hipgraph": replay / (65536 / SAMPLE_RATE),
                                  "graph_equals_eager": ok}
+        # one StreamingVocoder chunk (glue.py): 64 new frames + the receptive-field context
+        # (15 frames for V1) on each side, one utterance
+        ctx = gen.receptive_field_frames()
+        chunk = torch.randn(1, 80, 64 + 2 * ctx, generator=g).to(dev)
+        for _ in range(3):
+            gen(chunk)
+        t_chunk = timed(lambda: gen(chunk), 20)
+        out["streaming_chunk_v1_64f"] = {"frames_in": 64 + 2 * ctx, "frames_emitted": 64,
+                                         "ms": t_chunk * 1e3,
+                                         "rtf": t_chunk / (64 * 256 / SAMPLE_RATE)}
         del gen
         gen = make(S.V2STAR)
         mel = torch.randn(16, 80, 2048, generator=g).to(dev)
