@@ -317,7 +317,8 @@ def main():
         rank, world, local_rank = (int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"]),
                                    int(os.environ.get("LOCAL_RANK", "0")))
     pmc, pmc_note = None, "not collected (--no-pmc or N > 1)"
-    if world == 1 and not args.no_pmc and not args.pmc_child:
+    under_profiler = "rocprof" in os.environ.get("LD_PRELOAD", "")
+    if world == 1 and not args.no_pmc and not args.pmc_child and not under_profiler:
         # before this process initialises the GPU: the passes are child processes
         pmc, pmc_note = pmc_traffic(["--preset", args.preset, "--batch", str(args.batch),
                                      "--frames", str(args.frames), "--precision", args.precision])
