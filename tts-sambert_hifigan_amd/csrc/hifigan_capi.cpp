@@ -100,6 +100,11 @@ struct Stage {
   std::vector<int> thin_halo;    // per ResBlock receptive-field radius
   std::vector<size_t> thin_w_off;  // per conv, floats into the packed buffer ([tap][ci][co])
   size_t thin_b_off = 0;           // [conv][C]
+  // bf16x3: the MFMA kernel's A stream [conv][step][plane][lane][8] (mrf_thin_mfma.hip)
+  bool thin_mfma = false;
+  size_t thin_m_off = 0;           // floats into the packed buffer
+  size_t thin_m_bytes = 0;
+  std::vector<int> thin_m_conv;    // byte offset of each conv inside the stream
 };
 
 }  // namespace
@@ -136,6 +141,9 @@ struct hfg_handle {
   int ups_swizzle = 1;       // XCD swizzle of the upsampler blocks (HFG_UPS_SWIZZLE=0: off)
   int small_tile = -1;       // small-grid tile: -1 auto (grid < kSmallGridBlocks), 0 never,
                              // 1 always (HFG_SMALL_TILE)
+  int thin_mfma = -1;        // bf16x3 thin stages on mrf_thin_mfma: -1 auto (C = 16; the
+                             // C = 8 stage stays on the VALU kernel), 0 none, 1 every C
+                             // (HFG_THIN_MFMA)
   bool thin = true;          // whole-MRF VALU kernel for C <= 16 stages (HFG_THIN=0: layer
                              // kernels instead)
   bool c16 = false;          // 16x16x32-shape wide layer kernel conv16_bf16x3 (HFG_C16=1;
@@ -460,9 +468,47 @@ int build_layers(hfg_handle* h) {
     }
     st.thin_b_off = off;
     off += ((size_t)n_conv * C + 63) & ~(size_t)63;
+    // bf16x3: the MFMA variant when every conv's zero-padded last k-step stays in the
+    // operand margin
+    const int tps = 32 / C;
+    bool mf = h->cfg.dtype == HFG_DTYPE_BF16X3 && h->thin_mfma != 0 &&
+              (h->thin_mfma == 1 || C == 16) && hfg::thin_mfma_window(C) > 0 &&
+              hfg::thin_mfma_window(C) - 2 * halo_max >= hfg::thin_mfma_window(C) / 4;
+    size_t bytes = 0;
+    st.thin_m_conv.clear();
+    for (int cv : convs) {
+      const Layer& Lc = h->layers[cv];
+      const int steps = (Lc.k + tps - 1) / tps;
+      if (((steps * tps - 1) - (Lc.k - 1) / 2) * Lc.dil > hfg::kThinMarg ||
+          steps > hfg::kThinMfmaMaxSteps)
+        mf = false;
+      st.thin_m_conv.push_back((int)bytes);
+      bytes += (size_t)steps * 2048;
+    }
+    st.thin_mfma = mf;
+    if (mf) {
+      st.thin_m_off = off;
+      st.thin_m_bytes = bytes;
+      off += (bytes / 4 + 63) & ~(size_t)63;
+    }
   }
   h->packed_host.assign(off, 0.f);
   return HFG_OK;
+}
+
+// float -> bf16, round to nearest even (NaN stays NaN)
+inline uint16_t f2bf(float f) {
+  uint32_t u;
+  memcpy(&u, &f, 4);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return (uint16_t)((u >> 16) | 0x40u);
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return (uint16_t)(u >> 16);
+}
+inline float bf2f(uint16_t b) {
+  uint32_t u = (uint32_t)b << 16;
+  float f;
+  memcpy(&f, &u, 4);
+  return f;
 }
 
 // mrf_thin weights: per conv [tap][ci][co] fp32 (the C output channels of one (tap, ci)
@@ -479,6 +525,44 @@ void pack_thin(hfg_handle* h, const Stage& st) {
           dst[((size_t)j * C + ci) * C + co] = w[((size_t)co * C + ci) * L.k + j];
     const float* bsrc = h->params[L.mod + ".bias"].data.data();
     for (int co = 0; co < C; ++co) h->packed_host[st.thin_b_off + e * C + co] = bsrc[co];
+  }
+  if (!st.thin_mfma) return;
+  // mrf_thin_mfma A stream: per (conv, k-step) [plane][lane][8] bf16, lane l -> row
+  // r = l & 15, K = 8 * (l >> 4) + e.  C = 16: plane 0 = hi, 1 = lo of w[r][ci][tap],
+  // ci = 8 ((l >> 4) & 1) + e, tap = 2 s + (l >> 5).  C = 8: ci = e, tap = 4 s + (l >> 4);
+  // plane 0 = [hi; lo] (rows 8-15 = lo of row - 8), plane 1 = [hi; 0].
+  uint16_t* dst = reinterpret_cast<uint16_t*>(h->packed_host.data() + st.thin_m_off);
+  const int tps = 32 / C;
+  for (size_t e = 0; e < st.thin_convs.size(); ++e) {
+    const Layer& L = h->layers[st.thin_convs[e]];
+    const float* w = h->params[L.mod + ".weight"].data.data();  // [C_out][C_in][k]
+    const int steps = (L.k + tps - 1) / tps;
+    uint16_t* de = dst + st.thin_m_conv[e] / 2;
+    for (int s = 0; s < steps; ++s)
+      for (int plane = 0; plane < 2; ++plane)
+        for (int lane = 0; lane < 64; ++lane)
+          for (int el = 0; el < 8; ++el) {
+            const int r = lane & 15, qq = lane >> 4;
+            int co, ci, tap;
+            bool lo_row = false;
+            if (C == 16) {
+              co = r;
+              ci = 8 * (qq & 1) + el;
+              tap = 2 * s + (qq >> 1);
+            } else {
+              co = r & 7;
+              lo_row = r >= 8;
+              ci = el;
+              tap = 4 * s + qq;
+            }
+            const float v = tap < L.k ? w[((size_t)co * C + ci) * L.k + tap] : 0.f;
+            const uint16_t hi = f2bf(v);
+            const uint16_t lo = f2bf(v - bf2f(hi));
+            uint16_t out;
+            if (C == 16) out = plane == 0 ? hi : lo;
+            else out = plane == 0 ? (lo_row ? lo : hi) : (lo_row ? (uint16_t)0 : hi);
+            de[((size_t)(s * 2 + plane) * 64 + lane) * 8 + el] = out;
+          }
   }
 }
 
@@ -504,20 +588,6 @@ void pack_gemm_weights(const Layer& L, F wt, float* dst) {
               }
 }
 
-// float -> bf16, round to nearest even (NaN stays NaN)
-inline uint16_t f2bf(float f) {
-  uint32_t u;
-  memcpy(&u, &f, 4);
-  if ((u & 0x7fffffffu) > 0x7f800000u) return (uint16_t)((u >> 16) | 0x40u);
-  u += 0x7fffu + ((u >> 16) & 1u);
-  return (uint16_t)(u >> 16);
-}
-inline float bf2f(uint16_t b) {
-  uint32_t u = (uint32_t)b << 16;
-  float f;
-  memcpy(&f, &u, 4);
-  return f;
-}
 
 // A-fragment order of conv1d_bf16x3 (conv_bf16x3.hip), in bf16 elements:
 //   idx = ((((((mt*n_g + g)*n_tg + tg)*TPC + jj)*2 + plane)*WAVES_M + wave_m)*WM + wm)*512
@@ -1107,13 +1177,21 @@ int run_thin(hfg_handle* h, Launcher& ln, const Stage& st, const float* X, int64
   // the kernel indexes biases as [conv][C] from this launch's first conv
   p.bias = h->packed_dev + st.thin_b_off + (size_t)cv_base * C;
   p.halo = halo;
-  p.W = hfg::thin_window(C) - 2 * halo;
+  p.W = (st.thin_mfma ? hfg::thin_mfma_window(C) : hfg::thin_window(C)) - 2 * halo;
   p.y = out;
   p.div = (float)p.n_res;
+  if (st.thin_mfma) {
+    const int base = st.thin_m_conv[cv_base];
+    p.wm = reinterpret_cast<const __bf16*>(h->packed_dev + st.thin_m_off) + base / 2;
+    p.wm_bytes = (int)st.thin_m_bytes - base;
+    for (int e = st.thin_conv0[j0]; e < st.thin_conv0[j1]; ++e)
+      p.wm_off[e - cv_base] = st.thin_m_conv[e] - base;
+  }
   const double bytes = 8.0 * B * Lt * C + wbytes;  // x once, y once, weights once
   const char* name = nullptr;
   ln.begin(flop, bytes);
-  hipError_t e = hfg::launch_mrf_thin(C, p, (int)B, ln.stream, &name);
+  hipError_t e = st.thin_mfma ? hfg::launch_mrf_thin_mfma(C, p, (int)B, ln.stream, &name)
+                               : hfg::launch_mrf_thin(C, p, (int)B, ln.stream, &name);
   ln.end(name);
   if (e != hipSuccess) return fail(HFG_EIO, "launch mrf_thin (C=%d): %s", C, hipGetErrorString(e));
   return HFG_OK;
@@ -1392,6 +1470,7 @@ int create_impl(const hfg_config* cfg, bool mrf_only, int device, hfg_handle** o
   if (const char* fe = getenv("HFG_FUSED_RB")) h->use_fused_rb = atoi(fe) != 0;
   if (const char* me = getenv("HFG_MFMA16")) h->mfma16 = atoi(me) != 0;
   if (const char* te = getenv("HFG_THIN")) h->thin = atoi(te) != 0;
+  if (const char* tm = getenv("HFG_THIN_MFMA")) h->thin_mfma = atoi(tm);
   if (const char* st = getenv("HFG_SMALL_TILE")) h->small_tile = atoi(st);
   if (const char* rc = getenv("HFG_RB_CONC")) h->rb_conc = atoi(rc);
   if (const char* us = getenv("HFG_UPS_SWIZZLE")) h->ups_swizzle = atoi(us);

@@ -212,11 +212,23 @@ struct ThinParams {
   int halo, W;               // largest ResBlock radius, output columns per block
   float* y;                  // [B][C][L] <- (sum of the ResBlocks' outputs) / div
   float div;
+  // bf16x3 MFMA variant (mrf_thin_mfma.hip): A stream [conv][step][plane][lane][8] bf16
+  const __bf16* wm;          // this launch's stream
+  int wm_bytes;              // its size (buffer descriptor range)
+  int wm_off[kThinMaxConv];  // byte offset of each conv's first k-step
 };
 int thin_window(int C);      // window columns of the C-channel instance (0: unsupported C)
 size_t thin_lds_bytes(int C);
 hipError_t launch_mrf_thin(int C, const ThinParams& p, int batch, hipStream_t stream,
                            const char** name);
+// the same MRF on the bf16 matrix cores in split precision (v_mfma_f32_16x16x32_bf16):
+// 4 waves x kThinMfmaTiles 16-column tiles (a 512-column window), C in {8, 16}
+constexpr int kThinMfmaTiles = 8;
+constexpr int kThinMfmaMaxSteps = 4;  // k-steps per conv (k <= 7 for C = 16, <= 15 for C = 8)
+int thin_mfma_window(int C);  // 0: unsupported C
+size_t thin_mfma_lds_bytes(int C);
+hipError_t launch_mrf_thin_mfma(int C, const ThinParams& p, int batch, hipStream_t stream,
+                                const char** name);
 
 // Launch the conv kernel for (tile, taps, ups).  Returns a hipError_t and,
 // via *name, the kernel's template-instance name (as rocprofv3 prints it).
