@@ -116,3 +116,23 @@ def test_concurrent_resblocks_hipgraph(pkg, dev):
         g.replay()
         torch.cuda.synchronize()
     assert torch.equal(out, eager)
+
+
+@pytest.mark.parametrize("precision", ["bf16x3"])
+def test_lds_staged_epilogue_is_bitwise_invisible(pkg, dev, precision):
+    """HFG_EPI_LDS=1: the bf16x3 layer kernels' epilogue staged through LDS with float4
+    stores (epilogue.h conv_epilogue_lds) — the same additions in the same order as the
+    accumulator-layout epilogue, so the wav is bitwise unchanged (residual, lrelu and MRF
+    running-sum modes all occur in a V1 forward)."""
+    from oracle import config as C
+    cfg = C.V1
+    sd = C.make_state_dict(cfg, seed=35)
+    mel = torch.randn(2, 80, 200, generator=torch.Generator().manual_seed(9))
+    outs = {}
+    for mode in ("0", "1"):
+        gen = _gen(pkg, cfg, sd, dev, precision, {"HFG_EPI_LDS": mode, "HFG_SMALL_TILE": "0",
+                                                  "HFG_RB_CONC": "0"})
+        with torch.no_grad():
+            outs[mode] = gen(mel.to(dev), lengths=[200, 141])
+        torch.cuda.synchronize()
+    assert torch.equal(outs["0"], outs["1"])

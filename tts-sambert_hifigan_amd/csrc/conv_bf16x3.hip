@@ -20,6 +20,8 @@
 // is multiplied), one barrier per chunk.  Epilogue identical to conv1d_mfma_f32.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include <cstdio>
 #include <type_traits>
 
@@ -499,8 +501,17 @@ conv1d_bf16x3(const ConvParams p) {
       }
     }
   } else {
-    conv_epilogue<WM, WN>(p, acc, b, mt * MT + wave_m * 32 * WM, n0 + wave_n * 32 * WN, N_b,
-                          half, col);
+    // LDS-staged float4 epilogue (epilogue.h) when the rows are 16-B aligned and the host
+    // sized the LDS for it (p.epi_lds); the accumulator-layout epilogue otherwise
+    if (p.epi_lds && (p.N & 3) == 0) {
+      lds_barrier();  // every wave is done with the weight slabs and input windows
+      float* stage = reinterpret_cast<float*>(lds16) + wave * 32 * (32 * WN + 8);
+      conv_epilogue_lds<WM, WN>(p, acc, b, mt * MT + wave_m * 32 * WM, n0 + wave_n * 32 * WN,
+                                N_b, half, col, stage, lane);
+    } else {
+      conv_epilogue<WM, WN>(p, acc, b, mt * MT + wave_m * 32 * WM, n0 + wave_n * 32 * WN, N_b,
+                            half, col);
+    }
   }
 }
 
@@ -563,7 +574,9 @@ hipError_t launch_conv_bf16x3(int tile, int kt, bool ups, const ConvParams& p, i
   if (!e->name[0])
     snprintf(e->name, sizeof(e->name), "conv1d_bf16x3<%d, %d, %d, %d, %d, %d, %d, %s>", e->kt,
              t.TPC, t.WAVES_M, t.WAVES_N, t.WM, t.WN, t.WD, e->ups ? "true" : "false");
-  const size_t lds = bf16x3_lds_bytes(tile, kt, p.dil);
+  size_t lds = bf16x3_lds_bytes(tile, kt, p.dil);
+  if (p.epi_lds && !ups)
+    lds = std::max(lds, (size_t)t.threads() / 64 * 32 * (32 * t.WN + 8) * sizeof(float));
   if (lds > 160 * 1024) return hipErrorInvalidValue;
   if (!e->attr) {
     hipError_t err = hipFuncSetAttribute(reinterpret_cast<const void*>(e->fn),

@@ -93,4 +93,116 @@ __device__ __forceinline__ void conv_epilogue(const ConvParams& p, floatx16e (&a
   conv_epilogue<WM, WN>(p, p.bias, acc, b, row_base, n_base, N_b, half, col);
 }
 
+// The same contract with the tile staged through LDS: each wave writes 32 accumulator
+// rows x 32*WN columns at a time into its own LDS region (row stride 32*WN + 8 floats:
+// the two row quads a ds_write_b32 touches land 32 banks apart) and reads them back as
+// row-contiguous float4, so the residual / MRF loads and the stores are 16-B per lane
+// and fully coalesced (4x fewer memory instructions than the accumulator layout's
+// one-dword-per-row stores).  Needs N % 4 == 0 (16-B aligned rows) and
+// 32 * (32*WN + 8) * 4 bytes of LDS per wave at `stage`; the caller has barriered the
+// block (every wave is done with the main loop's LDS).
+template <int WM, int WN>
+__device__ __forceinline__ void conv_epilogue_lds(const ConvParams& p, floatx16e (&acc)[WM][WN],
+                                                  int b, int row_base, int n_base, int N_b,
+                                                  int half, int col, float* stage, int lane) {
+  constexpr int SROW = 32 * WN + 8;
+  constexpr int C4 = 8 * WN;                 // float4 per staged row
+  const int64_t bo = (int64_t)b * p.y_bs;
+  const float* resb = p.res ? p.res + bo : nullptr;
+  float* outb = (p.mrf ? p.mrf : p.y) + bo;
+  const bool add_mrf = p.mrf && (p.mrf_mode & 1);
+  const bool div_mrf = p.mrf && (p.mrf_mode & 2);
+  const bool act = p.act_out != 0;
+#pragma unroll
+  for (int i = 0; i < WM; ++i) {
+#pragma unroll
+    for (int k = 0; k < WN; ++k)
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        stage[((r & 3) + 8 * (r >> 2) + 4 * half) * SROW + k * 32 + col] = acc[i][k][r];
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's writes are in LDS
+    __builtin_amdgcn_wave_barrier();
+    constexpr int IT = 32 * C4 / 64;          // float4 per lane
+#pragma unroll
+    for (int it0 = 0; it0 < IT; it0 += 4) {
+      float4 v[4];
+      int row[4], n[4];
+      bool ok[4], full[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int e = (it0 + u) * 64 + lane;
+        const int rr = e / C4, c4 = e - rr * C4;
+        row[u] = row_base + i * 32 + rr;
+        n[u] = n_base + 4 * c4;
+        ok[u] = row[u] < p.M && n[u] < N_b;
+        full[u] = ok[u] && n[u] + 3 < N_b;
+        v[u] = *reinterpret_cast<const float4*>(stage + rr * SROW + 4 * c4);
+        const float bv = p.bias[row[u]];
+        v[u].x += bv;
+        v[u].y += bv;
+        v[u].z += bv;
+        v[u].w += bv;
+      }
+      if (resb) {
+        float4 rv[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          rv[u] = ok[u] ? *reinterpret_cast<const float4*>(resb + (int64_t)row[u] * p.N + n[u])
+                        : float4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          v[u].x = rv[u].x + v[u].x;
+          v[u].y = rv[u].y + v[u].y;
+          v[u].z = rv[u].z + v[u].z;
+          v[u].w = rv[u].w + v[u].w;
+        }
+      }
+      if (act) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          v[u].x = v[u].x > 0.f ? v[u].x : v[u].x * kLReluSlope;
+          v[u].y = v[u].y > 0.f ? v[u].y : v[u].y * kLReluSlope;
+          v[u].z = v[u].z > 0.f ? v[u].z : v[u].z * kLReluSlope;
+          v[u].w = v[u].w > 0.f ? v[u].w : v[u].w * kLReluSlope;
+        }
+      }
+      if (add_mrf) {
+        float4 mv[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          mv[u] = ok[u] ? *reinterpret_cast<const float4*>(outb + (int64_t)row[u] * p.N + n[u])
+                        : float4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          v[u].x = mv[u].x + v[u].x;
+          v[u].y = mv[u].y + v[u].y;
+          v[u].z = mv[u].z + v[u].z;
+          v[u].w = mv[u].w + v[u].w;
+        }
+      }
+      if (div_mrf) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          v[u].x = v[u].x / p.mrf_div;
+          v[u].y = v[u].y / p.mrf_div;
+          v[u].z = v[u].z / p.mrf_div;
+          v[u].w = v[u].w / p.mrf_div;
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        float* dst = outb + (int64_t)row[u] * p.N + n[u];
+        if (full[u]) {
+          *reinterpret_cast<float4*>(dst) = v[u];
+        } else if (ok[u]) {
+          dst[0] = v[u].x;
+          if (n[u] + 1 < N_b) dst[1] = v[u].y;
+          if (n[u] + 2 < N_b) dst[2] = v[u].z;
+        }
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
 }  // namespace hfg

@@ -139,6 +139,7 @@ struct hfg_handle {
                              // (HFG_RB_WN32: 4 or 8)
   bool mfma16 = true;        // 16x16x32-shape ResBlock kernel for C = 32 (HFG_MFMA16=0: off)
   int ups_swizzle = 1;       // XCD swizzle of the upsampler blocks (HFG_UPS_SWIZZLE=0: off)
+  int epi_lds = 1;           // LDS-staged float4 epilogue of the bf16x3 layer convs (HFG_EPI_LDS=0: off)
   int small_tile = -1;       // small-grid tile: -1 auto (grid < kSmallGridBlocks), 0 never,
                              // 1 always (HFG_SMALL_TILE)
   int thin_mfma = -1;        // bf16x3 thin stages on mrf_thin_mfma: -1 auto (C = 16; the
@@ -1022,6 +1023,7 @@ int run_conv(hfg_handle* h, Launcher& ln, const Layer& L, const float* x, int64_
   p.mrf_div = mrf_div;
   p.n_chunks = L.n_chunks;
   p.dbg = h->dbg_flags;
+  p.epi_lds = h->epi_lds;
   const int ntile = L.tile == hfg::kWsTile    ? hfg::kWsNT
                     : L.tile == hfg::kC16Tile ? hfg::kC16NT
                     : L.prec == 1             ? hfg::kBf16x3Tiles[L.tile].NTILE()
@@ -1474,6 +1476,7 @@ int create_impl(const hfg_config* cfg, bool mrf_only, int device, hfg_handle** o
   if (const char* st = getenv("HFG_SMALL_TILE")) h->small_tile = atoi(st);
   if (const char* rc = getenv("HFG_RB_CONC")) h->rb_conc = atoi(rc);
   if (const char* us = getenv("HFG_UPS_SWIZZLE")) h->ups_swizzle = atoi(us);
+  if (const char* el = getenv("HFG_EPI_LDS")) h->epi_lds = atoi(el);
   if (const char* ce = getenv("HFG_C16")) h->c16 = atoi(ce) != 0;
   if (const char* se = getenv("HFG_SPLIT")) h->split = atoi(se);
   if (const char* rn = getenv("HFG_RB64_NARROW")) h->rb64_narrow = atoi(rn) != 0;

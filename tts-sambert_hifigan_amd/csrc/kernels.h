@@ -38,6 +38,7 @@ struct ConvParams {
   int ups_swz;              // UPS: XCD swizzle of the block order (bf16x3 kernel)
   int n_chunks;      // ceil(C_in / CK)
   int n_base;        // first GEMM column of this launch (bf16x3 kernel; 0 elsewhere)
+  int epi_lds;       // bf16x3 layer kernel: LDS-staged float4 epilogue (epilogue.h)
   int dbg;           // ablation flags (HFG_DEBUG_FLAGS; 0 in production; wrong results when
                      // set), bf16x3 kernel: bit0 skip input restaging after the first
                      // chunk, bit2 no per-chunk barrier, bit3 no epilogue
