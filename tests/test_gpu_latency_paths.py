@@ -118,7 +118,7 @@ def test_concurrent_resblocks_hipgraph(pkg, dev):
     assert torch.equal(out, eager)
 
 
-@pytest.mark.parametrize("precision", ["bf16x3"])
+@pytest.mark.parametrize("precision", ["bf16x3", "fp32"])
 def test_lds_staged_epilogue_is_bitwise_invisible(pkg, dev, precision):
     """HFG_EPI_LDS=1: the bf16x3 layer kernels' epilogue staged through LDS with float4
     stores (epilogue.h conv_epilogue_lds) — the same additions in the same order as the

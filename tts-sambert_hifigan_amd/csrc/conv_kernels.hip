@@ -222,6 +222,12 @@ conv1d_mfma_f32(const ConvParams p) {
         }
       }
     }
+  } else if (p.epi_lds && (p.N & 3) == 0) {
+    // LDS-staged float4 epilogue (epilogue.h; the host sized the LDS for it)
+    __syncthreads();  // every wave is done with the main loop's LDS
+    conv_epilogue_lds<WM, WN>(p, acc, b, mt * MT + wave_m * 32 * WM, n0 + wave_n * 32 * WN, N_b,
+                              half, col, lds + (threadIdx.x >> 6) * 32 * (32 * WN + 8),
+                              threadIdx.x & 63);
   } else {
     conv_epilogue<WM, WN>(p, acc, b, mt * MT + wave_m * 32 * WM, n0 + wave_n * 32 * WN, N_b,
                           half, col);
@@ -349,7 +355,11 @@ hipError_t launch_conv(TileId tile, int kt, bool ups, const ConvParams& p, int n
   if ((kt - 1) * p.dil > halo_max(e->kt)) return hipErrorInvalidValue;
   const int xw = t.NTILE() + (kt - 1) * p.dil;
   const size_t stage = (size_t)t.MT() * ck * kt + (((size_t)ck * xw + 3) & ~(size_t)3);
-  const size_t lds = sizeof(float) * 2 * stage;
+  size_t lds = sizeof(float) * 2 * stage;
+  // the LDS-staged epilogue only where its staging fits the main loop's footprint
+  ConvParams pe = p;
+  const size_t epi = sizeof(float) * (size_t)t.threads() / 64 * 32 * (32 * t.WN + 8);
+  if (ups || epi > lds) pe.epi_lds = 0;
   if (lds > 160 * 1024) return hipErrorInvalidValue;
   if (lds > 64 * 1024 && !e->lds_attr_set) {
     hipError_t err = hipFuncSetAttribute(reinterpret_cast<const void*>(e->fn),
@@ -359,7 +369,7 @@ hipError_t launch_conv(TileId tile, int kt, bool ups, const ConvParams& p, int n
   }
   if (name) *name = e->name;
   dim3 grid(n_tiles, m_tiles, batch);
-  e->fn<<<grid, dim3(t.threads()), lds, stream>>>(p);
+  e->fn<<<grid, dim3(t.threads()), lds, stream>>>(pe);
   return hipGetLastError();
 }
 
