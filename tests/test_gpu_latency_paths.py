@@ -136,3 +136,4 @@ def test_lds_staged_epilogue_is_bitwise_invisible(pkg, dev, precision):
             outs[mode] = gen(mel.to(dev), lengths=[200, 141])
         torch.cuda.synchronize()
     assert torch.equal(outs["0"], outs["1"])
+

@@ -504,7 +504,11 @@ conv1d_bf16x3(const ConvParams p) {
     // LDS-staged float4 epilogue (epilogue.h) when the rows are 16-B aligned and the host
     // sized the LDS for it (p.epi_lds); the accumulator-layout epilogue otherwise
     if (p.epi_lds && (p.N & 3) == 0) {
-      lds_barrier();  // every wave is done with the weight slabs and input windows
+      // every wave is done with the weight slabs and input windows, and no weight-slab
+      // LDS-DMA is still in flight (a deeper ring leaves the re-read past-the-end slabs
+      // outstanding; they count in vmcnt, not lgkmcnt)
+      wait_vm<0>();
+      lds_barrier();
       float* stage = reinterpret_cast<float*>(lds16) + wave * 32 * (32 * WN + 8);
       conv_epilogue_lds<WM, WN>(p, acc, b, mt * MT + wave_m * 32 * WM, n0 + wave_n * 32 * WN,
                                 N_b, half, col, stage, lane);

@@ -224,7 +224,9 @@ conv1d_mfma_f32(const ConvParams p) {
     }
   } else if (p.epi_lds && (p.N & 3) == 0) {
     // LDS-staged float4 epilogue (epilogue.h; the host sized the LDS for it)
-    __syncthreads();  // every wave is done with the main loop's LDS
+    // every wave is done with the main loop's LDS and no weight LDS-DMA is in flight
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
     conv_epilogue_lds<WM, WN>(p, acc, b, mt * MT + wave_m * 32 * WM, n0 + wave_n * 32 * WN, N_b,
                               half, col, lds + (threadIdx.x >> 6) * 32 * (32 * WN + 8),
                               threadIdx.x & 63);

@@ -416,7 +416,10 @@ int build_layers(hfg_handle* h) {
         rb.halo += (rb.kt - 1) / 2 * c.dil[j][m] + (rb.kt - 1) / 2;
         if ((rb.kt - 1) / 2 * c.dil[j][m] > hfg::rb_marg(C, waves_n)) ok = false;
       }
-      rb.W = nwin - 2 * rb.halo;
+      // a multiple of 4: block origins t0 = W * blockIdx stay 16-B aligned for the
+      // LDS-staged float4 MRF epilogue (which column a block computes does not change
+      // its arithmetic: bitwise the same result for any W)
+      rb.W = (nwin - 2 * rb.halo) & ~3;
       if (rb.W < nwin / 4) ok = false;
       if (C == 128 && (double)nwin / rb.W > 1.15) ok = false;
       if (!ok) continue;
