@@ -115,12 +115,18 @@ def _host_cores():
     sched_getaffinity but grants a share of them)."""
     aff = len(os.sched_getaffinity(0))
     quota = None
-    try:
+    try:  # cgroup v2
         q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
         if q != "max":
             quota = max(1, int(int(q) / int(per)))
     except Exception:
-        quota = None
+        try:  # cgroup v1
+            q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+            per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+            if q > 0:
+                quota = max(1, q // per)
+        except Exception:
+            quota = None
     model = ""
     try:
         for line in open("/proc/cpuinfo"):
