@@ -58,9 +58,13 @@ PEAK_BF16_TFLOPS = 2500.0  # MI355X_MICROARCH.md: BF16 MFMA dense (no sparsity)
 
 def kernel_peak(name: str):
     """(peak in algorithmic fp32-conv TFLOP/s, description) for one kernel."""
-    if "bf16x3" in name:  # conv1d_bf16x3, resblock[16]_bf16x3, conv_ws_bf16x3
-        # 3 bf16 MFMA products (hi*hi + hi*lo + lo*hi) per algorithmic multiply-add
-        return PEAK_BF16_TFLOPS / 3.0, "bf16 dense MFMA 2.5 PFLOP/s / 3 split products"
+    if "bf16x3" in name or "mrf_thin_mfma" in name:
+        # conv1d_bf16x3, resblock[16]_bf16x3, conv_ws_bf16x3, mrf_thin_mfma: 3 bf16 MFMA
+        # products (hi*hi + hi*lo + lo*hi) per algorithmic multiply-add, 2 for the bf16w
+        # instances (last template argument NP = 2: lo(w) = 0 skipped)
+        np_ = 2 if name.replace(" ", "").split("(")[0].endswith(",2>") else 3
+        return (PEAK_BF16_TFLOPS / np_,
+                f"bf16 dense MFMA 2.5 PFLOP/s / {np_} split products")
     return PEAK_FP32_TFLOPS, "fp32 MFMA 157.3 TFLOP/s"
 
 
@@ -72,10 +76,12 @@ def parse():
     ap.add_argument("--preset", default="v1", choices=["v1", "v2star"])
     ap.add_argument("--batch", type=int, default=8, help="utterances per GPU")
     ap.add_argument("--frames", type=int, default=1024)
-    ap.add_argument("--precision", default="bf16x3", choices=["fp32", "bf16x3"],
+    ap.add_argument("--precision", default="bf16x3", choices=["fp32", "bf16x3", "bf16w"],
                     help="conv arithmetic: bf16x3 split-precision MFMA (default; parity 1e-4 "
-                         "met, tests/test_gpu_parity.py) or exact fp32 MFMA")
-    ap.add_argument("--also", nargs="*", default=["fp32"],
+                         "met, tests/test_gpu_parity.py), exact fp32 MFMA, or bf16w (weights "
+                         "stored as bf16: a different model, parity against the bf16-rounded "
+                         "weights, tests/test_gpu_bf16w.py)")
+    ap.add_argument("--also", nargs="*", default=["fp32", "bf16w"],
                     help="extra precisions measured in the same run (reported under 'alt')")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl = RCCL over xGMI (production); gloo only to rehearse N>1 on one GPU")
@@ -491,7 +497,7 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "f32" if args.precision == "fp32" else "bf16x3",
+        "dtype": "f32" if args.precision == "fp32" else args.precision,
         "dtype_note": ("fp32 operands on the fp32 MFMA (exact products)" if args.precision == "fp32"
                        else "fp32 in/out and fp32 accumulation; every fp32 operand split into bf16 "
                             "hi + lo, products hi*hi + hi*lo + lo*hi on the bf16 MFMA (the "
@@ -534,7 +540,9 @@ def main():
             entry = {"value": v, "ms_per_step": 1000.0 * el / args.steps,
                      "rtf": (el / args.steps) / (args.batch * ol / SAMPLE_RATE),
                      "speedup_vs_headline": v / value,
-                     "parity": "atol 1e-4 vs reference fixtures (tests/test_gpu_parity.py)"}
+                     "parity": ("atol 1e-4 vs the oracle run on the bf16-rounded weights "
+                                "(tests/test_gpu_bf16w.py)" if prec == "bf16w" else
+                                "atol 1e-4 vs reference fixtures (tests/test_gpu_parity.py)")}
             if pr:
                 entry["roofline"] = roofline(pr, prof_ms.get(prec, 1000.0 * el / args.steps))
                 entry["kernels"] = {k: {"launches": q["launches"] // args.steps,
@@ -576,13 +584,13 @@ def main():
         all_flop = sum(v["flop"] for v in prof.values()) / args.steps
         all_bytes = sum(v["bytes"] for v in prof.values()) / args.steps
         step_s = elapsed / args.steps
-        issue = 3.0 if args.precision == "bf16x3" else 1.0
+        issue = {"bf16x3": 3.0, "bf16w": 2.0}.get(args.precision, 1.0)
         line["roofline_step"] = {
             "compute_TFLOPs": all_flop / step_s / 1e12,
             "mfma_issue_frac": (all_flop * issue / step_s / 1e12 /
-                                (PEAK_BF16_TFLOPS if args.precision == "bf16x3" else PEAK_FP32_TFLOPS)),
-            "mfma_issue_note": ("algorithmic FLOP x 3 bf16 MFMA products per multiply-add / step "
-                                "time / 2.5 PF bf16 dense peak" if args.precision == "bf16x3" else
+                                (PEAK_BF16_TFLOPS if args.precision != "fp32" else PEAK_FP32_TFLOPS)),
+            "mfma_issue_note": (f"algorithmic FLOP x {issue:.0f} bf16 MFMA products per multiply-add "
+                                "/ step time / 2.5 PF bf16 dense peak" if args.precision != "fp32" else
                                 "algorithmic FLOP / step time / 157.3 TF fp32 MFMA peak"),
             "hbm_model_GBs": all_bytes / step_s / 1e9,
             "hbm_model_frac": all_bytes / step_s / 1e9 / PEAK_HBM_GBS,

@@ -73,9 +73,16 @@ extern "C" {
  *            whole-ResBlock kernels of the C = 32/64/128 stages and the layer convs
  *            of C >= 32; convs whose (k-1)*dilation exceeds the bf16x3 window fall
  *            back to the fp32 kernels.  Output within ~1e-5 of the reference at
- *            default weight scale (1e-4 bar; DESIGN.md §4 gives the x4-scale limit). */
+ *            default weight scale (1e-4 bar; DESIGN.md §4 gives the x4-scale limit).
+ *   BF16W  : bf16 weight storage — every conv weight rounded to bf16 (nearest-even)
+ *            when the weights are committed, activations still split hi/lo: hi*hi +
+ *            hi*lo on the bf16 matrix cores (2 MFMAs per multiply-add instead of 3),
+ *            exact products of the bf16-rounded weights elsewhere.  Output is that of
+ *            the reference Generator whose weights were cast to bf16 (1e-4 bar against
+ *            that model), not of the fp32-weight model.  Biases stay fp32. */
 #define HFG_DTYPE_FP32 0
 #define HFG_DTYPE_BF16X3 1
+#define HFG_DTYPE_BF16W 2
 
 typedef struct hfg_handle hfg_handle;
 

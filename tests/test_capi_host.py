@@ -478,3 +478,56 @@ def test_resblock_stream_packing_and_windowing(pkg, preset, m16, monkeypatch):
                 out[:, t0:t0 + (c1 - c0)] = yw[:, c0:c1]
             assert np.abs(out - direct).max() < 1e-9
     assert n_fused >= (7 if preset == "v1" else 1)
+
+
+def _bf16_rne(a):
+    """float32 → bf16 round-to-nearest-even, returned as float32 (numpy)."""
+    u = np.asarray(a, np.float32).view(np.uint32).astype(np.uint64)
+    r = ((u + 0x7FFF + ((u >> 16) & 1)) >> 16).astype(np.uint32) << 16
+    return r.view(np.float32)
+
+
+@pytest.mark.parametrize("big_tile", ["3", "4", "c16"])
+@pytest.mark.parametrize("preset", ["v1", "v2star"])
+def test_bf16w_packing(pkg, preset, big_tile, monkeypatch):
+    """HFG_DTYPE_BF16W: every conv weight is rounded to bf16 (nearest-even) when committed —
+    the split layers' lo planes are all zero and their hi planes are exactly bf16(W); the
+    fp32 layers (conv_post, C < 32 stages) hold the same bf16-valued weights; biases stay
+    fp32; the wide-tile / c16 variants (no NP 2 instances) are never chosen."""
+    monkeypatch.setenv("HFG_C16", "1" if big_tile == "c16" else "0")
+    monkeypatch.setenv("HFG_BF16X3_BIGTILE", "3" if big_tile == "c16" else big_tile)
+    cfg = C.PRESETS[preset]
+    sd = C.make_state_dict(cfg, seed=41)
+    h = host_handle(pkg, cfg, "bf16w")
+    for k, v in sd.items():
+        h.set_weight(k, torch.from_numpy(v))
+    h.commit()
+    h.commit()  # idempotent
+    n_split = n_fp32 = 0
+    for mod in ["conv_pre", "ups.0", "mrfs.0.resblocks.2.convs1.1", "mrfs.1.resblocks.0.convs2.1",
+                "mrfs.3.resblocks.2.convs2.1", "conv_post"]:
+        info, packed, bias = h.packed_layer(mod)
+        W = sd[mod + ".weight"]
+        if mod.startswith("ups."):  # bias repeated per polyphase row
+            assert set(np.unique(bias)) - {0.0} <= set(sd[mod + ".bias"]), mod
+        else:
+            assert np.array_equal(bias[:W.shape[0]], sd[mod + ".bias"]), mod
+        if info["CK"] == 16:
+            assert info["tile"] not in (8, 9), mod
+            n_split += 1
+            u = packed.view(np.uint16)
+            TPC = {0: 4, 1: 2, 2: 4, 3: 2, 4: 4}[info["tile"]]
+            planes = u.reshape(-1, TPC, 2, u.size // (info["m_tiles"] * info["n_chunks"] * TPC * 2))
+            assert not planes[:, :, 1].any(), f"{mod}: lo plane not zero"
+            hi = np.sort(bf2f(planes[:, :, 0]).ravel())
+            ref = np.sort(np.concatenate([_bf16_rne(W).ravel(),
+                                          np.zeros(hi.size - W.size, np.float32)]))
+            assert np.array_equal(hi, ref), mod
+        else:
+            n_fp32 += 1
+            vals = np.asarray(packed, np.float32)
+            assert not (vals.view(np.uint32) & 0xFFFF).any(), f"{mod}: weight not bf16-valued"
+            nz = np.sort(vals[vals != 0])
+            ref = _bf16_rne(W).ravel()
+            assert np.array_equal(nz, np.sort(ref[ref != 0])), mod
+    assert n_split >= 3 and n_fp32 >= 1

@@ -60,7 +60,7 @@ class HfgConfig(ctypes.Structure):
     ]
 
 
-DTYPES = {"fp32": 0, "bf16x3": 1}
+DTYPES = {"fp32": 0, "bf16x3": 1, "bf16w": 2}
 
 
 class HfgMrfConfig(ctypes.Structure):

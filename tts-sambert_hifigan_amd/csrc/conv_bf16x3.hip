@@ -36,7 +36,7 @@ typedef float floatx2 __attribute__((ext_vector_type(2)));
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 }  // namespace
 
-template <int KT_, int TPC, int WAVES_M, int WAVES_N, int WM, int WN, int WD, bool UPS>
+template <int KT_, int TPC, int WAVES_M, int WAVES_N, int WM, int WN, int WD, bool UPS, int NP>
 __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N, 2)
 conv1d_bf16x3(const ConvParams p) {
   constexpr int NW = WAVES_M * WAVES_N;
@@ -229,7 +229,8 @@ conv1d_bf16x3(const ConvParams p) {
     for (int i = 0; i < WM; ++i)
 #pragma unroll
       for (int k = 0; k < WN; ++k) {
-        acc[i][k] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.al[i], f.bh[k], acc[i][k], 0, 0, 0);
+        if constexpr (NP == 3)  // the weights' lo plane (zero for bf16-valued weights: NP 2)
+          acc[i][k] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.al[i], f.bh[k], acc[i][k], 0, 0, 0);
         acc[i][k] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.ah[i], f.bl[k], acc[i][k], 0, 0, 0);
         acc[i][k] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.ah[i], f.bh[k], acc[i][k], 0, 0, 0);
       }
@@ -259,7 +260,8 @@ conv1d_bf16x3(const ConvParams p) {
       if (k + 1 < WN) ldb(k + 1);
 #pragma unroll
       for (int i = 0; i < WM; ++i) {
-        acc[i][k] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[i], bh[k & 1], acc[i][k], 0, 0, 0);
+        if constexpr (NP == 3)
+          acc[i][k] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[i], bh[k & 1], acc[i][k], 0, 0, 0);
         acc[i][k] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bl[k & 1], acc[i][k], 0, 0, 0);
         acc[i][k] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bh[k & 1], acc[i][k], 0, 0, 0);
       }
@@ -273,12 +275,12 @@ conv1d_bf16x3(const ConvParams p) {
     constexpr bool LD = decltype(ld_tag)::value, ST = decltype(st_tag)::value;
     __builtin_amdgcn_sched_group_barrier(0x100, 2 * WM + 2, 0);
 #pragma unroll
-    for (int s = 0; s < 3 * WM * WN; ++s) {
+    for (int s = 0; s < NP * WM * WN; ++s) {
       __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
       __builtin_amdgcn_sched_group_barrier(0x002, NV, 0);
       if (LD) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
       if (ST && s % 4 == 3) __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);
-      if (s % (3 * WM) == 0 && s / (3 * WM) + 1 < WN)
+      if (s % (NP * WM) == 0 && s / (NP * WM) + 1 < WN)
         __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
     }
     __builtin_amdgcn_sched_barrier(0);
@@ -523,11 +525,11 @@ namespace {
 
 typedef void (*ConvFn3)(const ConvParams);
 
-template <int KT, int TILE, bool UPS>
+template <int KT, int TILE, bool UPS, int NP>
 struct Inst3 {
   static constexpr Bf16x3Cfg t = kBf16x3Tiles[TILE];
   static ConvFn3 fn() {
-    return conv1d_bf16x3<KT, t.TPC, t.WAVES_M, t.WAVES_N, t.WM, t.WN, t.WD, UPS>;
+    return conv1d_bf16x3<KT, t.TPC, t.WAVES_M, t.WAVES_N, t.WM, t.WN, t.WD, UPS, NP>;
   }
 };
 
@@ -535,17 +537,21 @@ struct Entry3 {
   int kt;
   int tile;
   bool ups;
+  int np;
   ConvFn3 fn;
   bool attr;
   char name[96];
 };
 
-#define HFG3_ENTRY(KT, TILE, UPS) \
-  { KT, TILE, UPS, Inst3<KT, TILE, UPS>::fn(), false, {0} }
-#define HFG3_TILES(KT, UPS)                                                              \
-  HFG3_ENTRY(KT, 0, UPS), HFG3_ENTRY(KT, 1, UPS), HFG3_ENTRY(KT, 2, UPS), HFG3_ENTRY(KT, 3, UPS), \
-      HFG3_ENTRY(KT, 4, UPS)
+#define HFG3_ENTRY(KT, TILE, UPS, NP) \
+  { KT, TILE, UPS, NP, Inst3<KT, TILE, UPS, NP>::fn(), false, {0} }
+#define HFG3_TILES(KT, UPS)                                                                  \
+  HFG3_ENTRY(KT, 0, UPS, 3), HFG3_ENTRY(KT, 1, UPS, 3), HFG3_ENTRY(KT, 2, UPS, 3),           \
+      HFG3_ENTRY(KT, 3, UPS, 3), HFG3_ENTRY(KT, 4, UPS, 3), HFG3_ENTRY(KT, 1, UPS, 2),       \
+      HFG3_ENTRY(KT, 2, UPS, 2), HFG3_ENTRY(KT, 3, UPS, 2), HFG3_ENTRY(KT, 4, UPS, 2)
 
+// NP 3: hi*hi + hi*lo + lo*hi (bf16x3); NP 2: hi*hi + hi*lo for bf16-valued weights
+// (HFG_DTYPE_BF16W: the weights' lo plane is zero), tiles 1-4
 Entry3 g_entries3[] = {
     HFG3_TILES(3, false), HFG3_TILES(5, false), HFG3_TILES(7, false), HFG3_TILES(11, false),
     HFG3_TILES(0, false), HFG3_TILES(2, true),  HFG3_TILES(0, true),
@@ -561,12 +567,13 @@ size_t bf16x3_lds_bytes(int tile, int kt, int dil) {
   return sizeof(__bf16) * (t.WD * slab + 2 * 2 * xplane);  // weight ring + 2 (hi,lo) windows
 }
 
-hipError_t launch_conv_bf16x3(int tile, int kt, bool ups, const ConvParams& p, int n_tiles,
-                              int m_tiles, int batch, hipStream_t stream, const char** name) {
+hipError_t launch_conv_bf16x3(int tile, int kt, bool ups, int np, const ConvParams& p,
+                              int n_tiles, int m_tiles, int batch, hipStream_t stream,
+                              const char** name) {
   Entry3* e = nullptr;
   Entry3* generic = nullptr;
   for (auto& cand : g_entries3) {
-    if (cand.tile != tile || cand.ups != ups) continue;
+    if (cand.tile != tile || cand.ups != ups || cand.np != np) continue;
     if (cand.kt == kt) e = &cand;
     if (cand.kt == 0) generic = &cand;
   }
@@ -576,8 +583,9 @@ hipError_t launch_conv_bf16x3(int tile, int kt, bool ups, const ConvParams& p, i
     return hipErrorInvalidValue;
   const Bf16x3Cfg& t = kBf16x3Tiles[tile];
   if (!e->name[0])
-    snprintf(e->name, sizeof(e->name), "conv1d_bf16x3<%d, %d, %d, %d, %d, %d, %d, %s>", e->kt,
-             t.TPC, t.WAVES_M, t.WAVES_N, t.WM, t.WN, t.WD, e->ups ? "true" : "false");
+    snprintf(e->name, sizeof(e->name), "conv1d_bf16x3<%d, %d, %d, %d, %d, %d, %d, %s, %d>",
+             e->kt, t.TPC, t.WAVES_M, t.WAVES_N, t.WM, t.WN, t.WD, e->ups ? "true" : "false",
+             e->np);
   size_t lds = bf16x3_lds_bytes(tile, kt, p.dil);
   if (p.epi_lds && !ups)
     lds = std::max(lds, (size_t)t.threads() / 64 * 32 * (32 * t.WN + 8) * sizeof(float));

@@ -64,6 +64,9 @@ struct Layer {
   size_t ws_off = 0, bs_off = 0;
 };
 
+// bf16x3 and bf16w both run the split-operand bf16 MFMA kernels
+inline bool split_dtype(int dtype) { return dtype == HFG_DTYPE_BF16X3 || dtype == HFG_DTYPE_BF16W; }
+
 struct Param {
   std::vector<int64_t> shape;
   std::vector<float> data;
@@ -139,6 +142,7 @@ struct hfg_handle {
                              // (HFG_RB_WN32: 4 or 8)
   bool mfma16 = true;        // 16x16x32-shape ResBlock kernel for C = 32 (HFG_MFMA16=0: off)
   int ups_swizzle = 1;       // XCD swizzle of the upsampler blocks (HFG_UPS_SWIZZLE=0: off)
+  int np = 3;                // MFMA products per multiply-add: 3 (bf16x3), 2 (bf16w: lo(w) = 0)
   int epi_lds = 1;           // LDS-staged float4 epilogue of the bf16x3 layer convs (HFG_EPI_LDS=0: off)
   int small_tile = -1;       // small-grid tile: -1 auto (grid < kSmallGridBlocks), 0 never,
                              // 1 always (HFG_SMALL_TILE)
@@ -187,8 +191,9 @@ int validate_config(const hfg_config* c) {
   if (c->n_mels <= 0) return fail(HFG_EINVAL, "n_mels must be > 0");
   if (c->n_up <= 0 || c->n_up > HFG_MAX_STAGES) return fail(HFG_EINVAL, "n_up out of range");
   if (c->n_res <= 0 || c->n_res > HFG_MAX_RES) return fail(HFG_EINVAL, "n_res out of range");
-  if (c->dtype != HFG_DTYPE_FP32 && c->dtype != HFG_DTYPE_BF16X3)
-    return fail(HFG_EINVAL, "dtype must be HFG_DTYPE_FP32 (0) or HFG_DTYPE_BF16X3 (1)");
+  if (c->dtype != HFG_DTYPE_FP32 && c->dtype != HFG_DTYPE_BF16X3 && c->dtype != HFG_DTYPE_BF16W)
+    return fail(HFG_EINVAL,
+                "dtype must be HFG_DTYPE_FP32 (0), HFG_DTYPE_BF16X3 (1) or HFG_DTYPE_BF16W (2)");
   if (c->c0 <= 0) return fail(HFG_EINVAL, "upsample_initial_channel must be > 0");
   for (int i = 0; i < c->n_up; ++i) {
     if (c->up_rates[i] <= 0 || c->up_kernels[i] <= 0)
@@ -310,7 +315,7 @@ int build_layers(hfg_handle* h) {
       off += 64;
       continue;
     }
-    if (h->cfg.dtype == HFG_DTYPE_BF16X3 && (L.kind == L_CONV || L.kind == L_UPS) &&
+    if (split_dtype(h->cfg.dtype) && (L.kind == L_CONV || L.kind == L_UPS) &&
         h->big_tile == hfg::kWsTile && hfg::ws_supported(L.KT, L.kind == L_UPS, L.M, L.dil)) {
       // warp-specialized path: A stream [m_tile][wave_m][group][tap][plane][lane][8]
       L.prec = 1;
@@ -326,7 +331,7 @@ int build_layers(hfg_handle* h) {
       off += (L.b_len + 63) & ~(size_t)63;
       continue;
     }
-    if (h->cfg.dtype == HFG_DTYPE_BF16X3 && (L.kind == L_CONV || L.kind == L_UPS) &&
+    if (split_dtype(h->cfg.dtype) && (L.kind == L_CONV || L.kind == L_UPS) &&
         h->c16 && h->big_tile == 3 && L.M >= 128 &&
         hfg::c16_supported(L.KT, L.kind == L_UPS, L.M, L.C_in, L.dil)) {
       // 16x16x32-shape wide layer kernel: A per k-step of two (group, tap) entries
@@ -343,7 +348,7 @@ int build_layers(hfg_handle* h) {
       off += (L.b_len + 63) & ~(size_t)63;
       continue;
     }
-    if (h->cfg.dtype == HFG_DTYPE_BF16X3 && (L.kind == L_CONV || L.kind == L_UPS) &&
+    if (split_dtype(h->cfg.dtype) && (L.kind == L_CONV || L.kind == L_UPS) &&
         hfg::bf16x3_tile_for_rows(L.M) >= 0 && hfg::bf16x3_supported(L.KT, L.dil)) {
       // split-precision path: chunk = 16 channels x TPC taps
       L.tile = hfg::bf16x3_tile_for_rows(L.M, h->big_tile == hfg::kWsTile ? 3 : h->big_tile);
@@ -395,7 +400,7 @@ int build_layers(hfg_handle* h) {
     Stage& st = h->stages[i];
     const int C = st.C;
     st.rbs.assign(c.n_res, RbFused{});
-    if (h->cfg.dtype != HFG_DTYPE_BF16X3 || !h->use_fused_rb || (C != 32 && C != 64 && C != 128))
+    if (!split_dtype(h->cfg.dtype) || !h->use_fused_rb || (C != 32 && C != 64 && C != 128))
       continue;
     int idx = 0;
     for (int j = 0; j < c.n_res; ++j) {
@@ -475,7 +480,7 @@ int build_layers(hfg_handle* h) {
     // bf16x3: the MFMA variant when every conv's zero-padded last k-step stays in the
     // operand margin
     const int tps = 32 / C;
-    bool mf = h->cfg.dtype == HFG_DTYPE_BF16X3 && h->thin_mfma != 0 &&
+    bool mf = split_dtype(h->cfg.dtype) && h->thin_mfma != 0 &&
               (h->thin_mfma == 1 || C == 16) && hfg::thin_mfma_window(C) > 0 &&
               hfg::thin_mfma_window(C) - 2 * halo_max >= hfg::thin_mfma_window(C) / 4;
     size_t bytes = 0;
@@ -834,6 +839,16 @@ void pack_layer(hfg_handle* h, const Layer& L) {
 int do_commit(hfg_handle* h) {
   for (auto& key : h->param_order)
     if (!h->params[key].set) return fail(HFG_EAGAIN, "weight '%s' was never set", key.c_str());
+  if (h->cfg.dtype == HFG_DTYPE_BF16W) {
+    // bf16 weight storage: every conv weight rounded to bf16 (round-to-nearest-even) in
+    // place, so every kernel (split planes: lo = 0; fp32 / VALU paths) sees the same
+    // bf16-valued weights; biases stay fp32.  Idempotent across commits.
+    for (auto& kv : h->params) {
+      const std::string& k = kv.first;
+      if (k.size() < 7 || k.compare(k.size() - 7, 7, ".weight") != 0) continue;
+      for (float& v : kv.second.data) v = bf2f(f2bf(v));
+    }
+  }
   std::fill(h->packed_host.begin(), h->packed_host.end(), 0.f);
   for (auto& L : h->layers) pack_layer(h, L);
   for (auto& st : h->stages) {
@@ -1046,7 +1061,7 @@ int run_conv(hfg_handle* h, Launcher& ln, const Layer& L, const float* x, int64_
                      ? hfg::launch_conv16_bf16x3(L.KT, false, p, n_tiles, L.m_tiles, (int)B,
                                                  ln.stream, &name)
                  : L.prec == 1
-                     ? hfg::launch_conv_bf16x3(tile, L.KT, false, p, n_tiles, m_tiles, (int)B,
+                     ? hfg::launch_conv_bf16x3(tile, L.KT, false, h->np, p, n_tiles, m_tiles, (int)B,
                                                ln.stream, &name)
                      : hfg::launch_conv((TileId)L.tile, L.KT, false, p, n_tiles, L.m_tiles,
                                         (int)B, ln.stream, &name);
@@ -1085,8 +1100,8 @@ int run_resblock(hfg_handle* h, Launcher& ln, const RbFused& rb, const float* x,
   const char* name = nullptr;
   ln.begin(flop, bytes);
   hipError_t e =
-      rb.m16 ? hfg::launch_resblock16_bf16x3(C, rb.waves_n, rb.kt, p, (int)B, ln.stream, &name)
-             : hfg::launch_resblock_bf16x3(C, rb.waves_n, rb.kt, p, (int)B, ln.stream, &name);
+      rb.m16 ? hfg::launch_resblock16_bf16x3(C, rb.waves_n, rb.kt, h->np, p, (int)B, ln.stream, &name)
+             : hfg::launch_resblock_bf16x3(C, rb.waves_n, rb.kt, h->np, p, (int)B, ln.stream, &name);
   ln.end(name);
   if (e != hipSuccess)
     return fail(HFG_EIO, "launch resblock %s: %s", L0.mod.c_str(), hipGetErrorString(e));
@@ -1139,7 +1154,7 @@ int run_ups(hfg_handle* h, Launcher& ln, const Layer& L, const float* x, int64_t
                      ? hfg::launch_conv16_bf16x3(L.KT, true, p, n_tiles, L.m_tiles, (int)B,
                                                  ln.stream, &name)
                  : L.prec == 1
-                     ? hfg::launch_conv_bf16x3(tile, L.KT, true, p, n_tiles, m_tiles, (int)B,
+                     ? hfg::launch_conv_bf16x3(tile, L.KT, true, h->np, p, n_tiles, m_tiles, (int)B,
                                                ln.stream, &name)
                      : hfg::launch_conv((TileId)L.tile, L.KT, true, p, n_tiles, L.m_tiles, (int)B,
                                         ln.stream, &name);
@@ -1195,7 +1210,7 @@ int run_thin(hfg_handle* h, Launcher& ln, const Stage& st, const float* X, int64
   const double bytes = 8.0 * B * Lt * C + wbytes;  // x once, y once, weights once
   const char* name = nullptr;
   ln.begin(flop, bytes);
-  hipError_t e = st.thin_mfma ? hfg::launch_mrf_thin_mfma(C, p, (int)B, ln.stream, &name)
+  hipError_t e = st.thin_mfma ? hfg::launch_mrf_thin_mfma(C, h->np, p, (int)B, ln.stream, &name)
                                : hfg::launch_mrf_thin(C, p, (int)B, ln.stream, &name);
   ln.end(name);
   if (e != hipSuccess) return fail(HFG_EIO, "launch mrf_thin (C=%d): %s", C, hipGetErrorString(e));
@@ -1486,6 +1501,13 @@ int create_impl(const hfg_config* cfg, bool mrf_only, int device, hfg_handle** o
   if (const char* we = getenv("HFG_RB_WN32")) {
     const int v = atoi(we);
     if (v == 4 || v == 8) h->rb_waves_n32 = v;
+  }
+  if (cfg->dtype == HFG_DTYPE_BF16W) {
+    // bf16-valued weights: their lo plane is zero, the kernels skip lo(w) * hi(x) (NP 2
+    // instances exist for the default tiles and the whole-ResBlock / thin kernels)
+    h->np = 2;
+    h->c16 = false;
+    if (h->big_tile != 3) h->big_tile = 3;
   }
   rc = build_layers(h);
   if (rc) {

@@ -127,8 +127,10 @@ size_t bf16x3_lds_bytes(int tile, int kt, int dil);
 inline bool bf16x3_supported(int kt, int dil) {
   return dil >= 1 && dil <= kMaxDil && kt >= 1 && kt <= 16 && (kt - 1) * dil <= kBf16x3MaxHalo;
 }
-hipError_t launch_conv_bf16x3(int tile, int kt, bool ups, const ConvParams& p, int n_tiles,
-                              int m_tiles, int batch, hipStream_t stream, const char** name);
+// np: MFMA products per multiply-add, 3 (bf16x3) or 2 (bf16-valued weights, tiles 1-4)
+hipError_t launch_conv_bf16x3(int tile, int kt, bool ups, int np, const ConvParams& p,
+                              int n_tiles, int m_tiles, int batch, hipStream_t stream,
+                              const char** name);
 
 // ---- warp-specialized bf16x3 conv (conv_ws_bf16x3.hip) ----
 // 128 x 256 block tile, 4 consumer waves (64 x 128 each) + 4 producer waves; weights
@@ -186,13 +188,13 @@ struct RbParams {
 };
 bool rb_supported(int C, int kt, int waves_n);
 size_t rb_lds_bytes(int C, int waves_n, int n_conv);
-hipError_t launch_resblock_bf16x3(int C, int waves_n, int kt, const RbParams& p, int batch,
-                                  hipStream_t stream, const char** name);
+hipError_t launch_resblock_bf16x3(int C, int waves_n, int kt, int np, const RbParams& p,
+                                  int batch, hipStream_t stream, const char** name);
 // the same on the 16x16x32 MFMA shape (resblock16_bf16x3.hip); A stream packed
 // [wave_m][conv][group32][tap][row tile][plane][lane][8]
 bool rb16_supported(int C, int kt, int waves_n);
-hipError_t launch_resblock16_bf16x3(int C, int waves_n, int kt, const RbParams& p, int batch,
-                                    hipStream_t stream, const char** name);
+hipError_t launch_resblock16_bf16x3(int C, int waves_n, int kt, int np, const RbParams& p,
+                                    int batch, hipStream_t stream, const char** name);
 
 // ---- whole MRF per launch for thin stages, C <= 16 (mrf_thin.hip) ----
 // All ResBlocks of one MRF on a time window in LDS, packed-fp32 VALU dot products (exact
@@ -228,8 +230,8 @@ constexpr int kThinMfmaTiles = 8;
 constexpr int kThinMfmaMaxSteps = 4;  // k-steps per conv (k <= 7 for C = 16, <= 15 for C = 8)
 int thin_mfma_window(int C);  // 0: unsupported C
 size_t thin_mfma_lds_bytes(int C);
-hipError_t launch_mrf_thin_mfma(int C, const ThinParams& p, int batch, hipStream_t stream,
-                                const char** name);
+hipError_t launch_mrf_thin_mfma(int C, int np, const ThinParams& p, int batch,
+                                hipStream_t stream, const char** name);
 
 // Launch the conv kernel for (tile, taps, ups).  Returns a hipError_t and,
 // via *name, the kernel's template-instance name (as rocprofv3 prints it).

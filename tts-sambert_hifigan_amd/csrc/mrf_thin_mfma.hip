@@ -45,7 +45,7 @@ typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 }  // namespace
 
-template <int C>
+template <int C, int NP>
 __global__ void __launch_bounds__(256, 2)
 mrf_thin_mfma(const ThinParams p) {
   static_assert(C == 16 || C == 8, "thin MFMA kernel: C in {8, 16}");
@@ -173,7 +173,8 @@ mrf_thin_mfma(const ThinParams p) {
         if (t + 1 < NCT) load_b((u + 1) & 1, s, t + 1);
         else if (s + 1 < steps) load_b((u + 1) & 1, s + 1, 0);
         if constexpr (C == 16) {
-          acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1[s], bh[u & 1], acc[t], 0, 0, 0);
+          if constexpr (NP == 3)  // the weights' lo plane (zero for bf16-valued weights)
+            acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1[s], bh[u & 1], acc[t], 0, 0, 0);
           acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0[s], bl[u & 1], acc[t], 0, 0, 0);
           acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0[s], bh[u & 1], acc[t], 0, 0, 0);
         } else {
@@ -252,18 +253,19 @@ namespace {
 typedef void (*ThinMfmaFn)(const ThinParams);
 
 struct EntryThinMfma {
-  int C;
+  int C, np;
   ThinMfmaFn fn;
   bool attr;
   char name[40];
 };
 
-EntryThinMfma g_entriesThinMfma[] = {{16, mrf_thin_mfma<16>, false, {0}},
-                                     {8, mrf_thin_mfma<8>, false, {0}}};
+EntryThinMfma g_entriesThinMfma[] = {{16, 3, mrf_thin_mfma<16, 3>, false, {0}},
+                                     {8, 3, mrf_thin_mfma<8, 3>, false, {0}},
+                                     {16, 2, mrf_thin_mfma<16, 2>, false, {0}}};
 
-EntryThinMfma* find_thin_mfma(int C) {
+EntryThinMfma* find_thin_mfma(int C, int np = 3) {
   for (auto& e : g_entriesThinMfma)
-    if (e.C == C) return &e;
+    if (e.C == C && (e.np == np || C == 8)) return &e;  // C = 8: 2 MFMAs per k-step anyway
   return nullptr;
 }
 
@@ -275,9 +277,9 @@ size_t thin_mfma_lds_bytes(int C) {
   return (size_t)2 * (4 * kThinMfmaTiles * 16 + 2 * kThinMarg) * 2 * C;
 }
 
-hipError_t launch_mrf_thin_mfma(int C, const ThinParams& p, int batch, hipStream_t stream,
-                                const char** name) {
-  EntryThinMfma* e = find_thin_mfma(C);
+hipError_t launch_mrf_thin_mfma(int C, int np, const ThinParams& p, int batch,
+                                hipStream_t stream, const char** name) {
+  EntryThinMfma* e = find_thin_mfma(C, np);
   if (!e) return hipErrorInvalidValue;
   const int nwin = thin_mfma_window(C);
   if (p.n_res < 1 || p.n_res > kThinMaxRes || !p.wm) return hipErrorInvalidValue;
@@ -301,7 +303,7 @@ hipError_t launch_mrf_thin_mfma(int C, const ThinParams& p, int batch, hipStream
     if (err != hipSuccess) return err;
     e->attr = true;
   }
-  if (!e->name[0]) snprintf(e->name, sizeof(e->name), "mrf_thin_mfma<%d>", e->C);
+  if (!e->name[0]) snprintf(e->name, sizeof(e->name), "mrf_thin_mfma<%d, %d>", e->C, e->np);
   if (name) *name = e->name;
   const int n_tiles = (p.L + p.W - 1) / p.W;
   e->fn<<<dim3(n_tiles, batch), dim3(256), lds, stream>>>(p);

@@ -39,7 +39,7 @@ typedef float floatx2 __attribute__((ext_vector_type(2)));
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 }  // namespace
 
-template <int KT, int WAVES_M, int WAVES_N>
+template <int KT, int WAVES_M, int WAVES_N, int NP>
 __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N, 2)  // 2 waves/SIMD: <= 256 VGPRs
 resblock16_bf16x3(const RbParams p) {
   constexpr int NW = WAVES_M * WAVES_N;
@@ -210,7 +210,8 @@ resblock16_bf16x3(const RbParams p) {
       }
 #pragma unroll
       for (int i = 0; i < WI; ++i) {
-        acc[i][k] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ra_l[SL][i], bh[k % NB], acc[i][k], 0, 0, 0);
+        if constexpr (NP == 3)  // the weights' lo plane (zero for bf16-valued weights: NP 2)
+          acc[i][k] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ra_l[SL][i], bh[k % NB], acc[i][k], 0, 0, 0);
         acc[i][k] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ra_h[SL][i], bl[k % NB], acc[i][k], 0, 0, 0);
         acc[i][k] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ra_h[SL][i], bh[k % NB], acc[i][k], 0, 0, 0);
       }
@@ -219,9 +220,9 @@ resblock16_bf16x3(const RbParams p) {
         __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // 1 DS read
         __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
         __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);  // rest of the unit's MFMAs
+        __builtin_amdgcn_sched_group_barrier(0x008, NP * WI - 2, 0);  // rest of the unit's MFMAs
       } else {
-        __builtin_amdgcn_sched_group_barrier(0x008, 6, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, NP * WI, 0);
       }
       if (k == WN - 1) {
         load_a(SL, qb + s + 2);  // this step's A fragments are dead
@@ -339,36 +340,38 @@ namespace {
 typedef void (*Rb16Fn)(const RbParams);
 
 struct EntryRb16 {
-  int kt, waves_m, waves_n;
+  int kt, waves_m, waves_n, np;
   Rb16Fn fn;
   bool attr;
   char name[64];
 };
 
-#define HFGRB16_ENTRY(KT, WMS, WNS) \
-  { KT, WMS, WNS, resblock16_bf16x3<KT, WMS, WNS>, false, {0} }
-#define HFGRB16_KTS(WMS, WNS)                                                         \
-  HFGRB16_ENTRY(3, WMS, WNS), HFGRB16_ENTRY(5, WMS, WNS), HFGRB16_ENTRY(7, WMS, WNS), \
-      HFGRB16_ENTRY(11, WMS, WNS)
+#define HFGRB16_ENTRY(KT, WMS, WNS, NP) \
+  { KT, WMS, WNS, NP, resblock16_bf16x3<KT, WMS, WNS, NP>, false, {0} }
+#define HFGRB16_KTS(WMS, WNS, NP)                                                           \
+  HFGRB16_ENTRY(3, WMS, WNS, NP), HFGRB16_ENTRY(5, WMS, WNS, NP),                         \
+      HFGRB16_ENTRY(7, WMS, WNS, NP), HFGRB16_ENTRY(11, WMS, WNS, NP)
 
-EntryRb16 g_entriesRb16[] = {HFGRB16_KTS(2, 4), HFGRB16_KTS(1, 8), HFGRB16_KTS(1, 4),
-                             HFGRB16_ENTRY(3, 4, 2)};
+// NP 3: bf16x3 products; NP 2: bf16-valued weights (HFG_DTYPE_BF16W)
+EntryRb16 g_entriesRb16[] = {HFGRB16_KTS(2, 4, 3), HFGRB16_KTS(1, 8, 3), HFGRB16_KTS(1, 4, 3),
+                             HFGRB16_ENTRY(3, 4, 2, 3), HFGRB16_KTS(2, 4, 2),
+                             HFGRB16_KTS(1, 8, 2), HFGRB16_KTS(1, 4, 2), HFGRB16_ENTRY(3, 4, 2, 2)};
 
 }  // namespace
 
 bool rb16_supported(int C, int kt, int waves_n) {
   if (C % 32 != 0) return false;
   for (auto& e : g_entriesRb16)
-    if (e.kt == kt && e.waves_m == C / 32 && e.waves_n == waves_n) return true;
+    if (e.kt == kt && e.waves_m == C / 32 && e.waves_n == waves_n && e.np == 3) return true;
   return false;
 }
 
-hipError_t launch_resblock16_bf16x3(int C, int waves_n, int kt, const RbParams& p, int batch,
-                                    hipStream_t stream, const char** name) {
+hipError_t launch_resblock16_bf16x3(int C, int waves_n, int kt, int np, const RbParams& p,
+                                    int batch, hipStream_t stream, const char** name) {
   const int wm = C / 32;
   EntryRb16* e = nullptr;
   for (auto& cand : g_entriesRb16)
-    if (cand.kt == kt && cand.waves_m == wm && cand.waves_n == waves_n) e = &cand;
+    if (cand.kt == kt && cand.waves_m == wm && cand.waves_n == waves_n && cand.np == np) e = &cand;
   if (!e || C % 32 != 0) return hipErrorInvalidValue;
   const int nwin = kRbColsPerWave * waves_n;
   if (p.n_conv < 2 || p.n_conv > kRbMaxConv || (p.n_conv & 1)) return hipErrorInvalidValue;
@@ -376,8 +379,8 @@ hipError_t launch_resblock16_bf16x3(int C, int waves_n, int kt, const RbParams& 
   for (int i = 0; i < p.n_conv; ++i)
     if (p.dil[i] < 1 || (kt - 1) / 2 * p.dil[i] > rb_marg(C, waves_n)) return hipErrorInvalidValue;
   if (!e->name[0])
-    snprintf(e->name, sizeof(e->name), "resblock16_bf16x3<%d, %d, %d>", e->kt, e->waves_m,
-             e->waves_n);
+    snprintf(e->name, sizeof(e->name), "resblock16_bf16x3<%d, %d, %d, %d>", e->kt, e->waves_m,
+             e->waves_n, e->np);
   const size_t lds = rb_lds_bytes(C, waves_n, p.n_conv);
   if (lds > 160 * 1024) return hipErrorInvalidValue;
   if (!e->attr) {

@@ -42,7 +42,7 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 typedef float floatx2 __attribute__((ext_vector_type(2)));
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 
-template <int KT, int WAVES_M, int WAVES_N>
+template <int KT, int WAVES_M, int WAVES_N, int NP>
 __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N, 2)  // 2 waves/SIMD: <= 256 VGPRs
 resblock_bf16x3(const RbParams p) {
   constexpr int NW = WAVES_M * WAVES_N;
@@ -204,7 +204,8 @@ resblock_bf16x3(const RbParams p) {
       if (s + 1 < STEPS) load_b(cur ^ 1, s + 1);
 #pragma unroll
       for (int k = 0; k < WN; ++k) {
-        acc[k] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ra_l[cur], bh[cur][k], acc[k], 0, 0, 0);
+        if constexpr (NP == 3)  // the weights' lo plane (zero for bf16-valued weights: NP 2)
+          acc[k] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ra_l[cur], bh[cur][k], acc[k], 0, 0, 0);
         acc[k] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ra_h[cur], bl[cur][k], acc[k], 0, 0, 0);
         acc[k] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ra_h[cur], bh[cur][k], acc[k], 0, 0, 0);
       }
@@ -218,7 +219,7 @@ resblock_bf16x3(const RbParams p) {
       }
       __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);    // 2 MFMA
       __builtin_amdgcn_sched_group_barrier(0x020, 2, 0);    // A loads
-      __builtin_amdgcn_sched_group_barrier(0x008, 3 * WN, 0);  // rest of the MFMAs
+      __builtin_amdgcn_sched_group_barrier(0x008, NP * WN, 0);  // rest of the MFMAs
       __builtin_amdgcn_sched_barrier(0);
     }
     lds_barrier();
@@ -283,20 +284,23 @@ namespace {
 typedef void (*RbFn)(const RbParams);
 
 struct EntryRb {
-  int kt, waves_m, waves_n;
+  int kt, waves_m, waves_n, np;
   RbFn fn;
   bool attr;
   char name[64];
 };
 
-#define HFGRB_ENTRY(KT, WMS, WNS) \
-  { KT, WMS, WNS, resblock_bf16x3<KT, WMS, WNS>, false, {0} }
-#define HFGRB_KTS(WMS, WNS)                                                             \
-  HFGRB_ENTRY(3, WMS, WNS), HFGRB_ENTRY(5, WMS, WNS), HFGRB_ENTRY(7, WMS, WNS), \
-      HFGRB_ENTRY(11, WMS, WNS)
+#define HFGRB_ENTRY(KT, WMS, WNS, NP) \
+  { KT, WMS, WNS, NP, resblock_bf16x3<KT, WMS, WNS, NP>, false, {0} }
+#define HFGRB_KTS(WMS, WNS, NP)                                                                 \
+  HFGRB_ENTRY(3, WMS, WNS, NP), HFGRB_ENTRY(5, WMS, WNS, NP), HFGRB_ENTRY(7, WMS, WNS, NP), \
+      HFGRB_ENTRY(11, WMS, WNS, NP)
 
-EntryRb g_entriesRb[] = {HFGRB_KTS(2, 4), HFGRB_KTS(1, 8), HFGRB_KTS(1, 4),
-                         HFGRB_ENTRY(3, 4, 2), HFGRB_ENTRY(3, 2, 2)};
+// NP 3: bf16x3 products; NP 2: bf16-valued weights (HFG_DTYPE_BF16W)
+EntryRb g_entriesRb[] = {HFGRB_KTS(2, 4, 3), HFGRB_KTS(1, 8, 3), HFGRB_KTS(1, 4, 3),
+                         HFGRB_ENTRY(3, 4, 2, 3), HFGRB_ENTRY(3, 2, 2, 3),
+                         HFGRB_KTS(2, 4, 2), HFGRB_KTS(1, 8, 2), HFGRB_KTS(1, 4, 2),
+                         HFGRB_ENTRY(3, 4, 2, 2), HFGRB_ENTRY(3, 2, 2, 2)};
 
 }  // namespace
 
@@ -305,7 +309,7 @@ bool rb_supported(int C, int kt, int waves_n) {
   const int wm = C / 32;
   if (C % 32 != 0) return false;
   for (auto& e : g_entriesRb)
-    if (e.kt == kt && e.waves_m == wm && e.waves_n == waves_n) return true;
+    if (e.kt == kt && e.waves_m == wm && e.waves_n == waves_n && e.np == 3) return true;
   return false;
 }
 
@@ -314,12 +318,12 @@ size_t rb_lds_bytes(int C, int waves_n, int n_conv) {
   return (size_t)C * rows * 4 + sizeof(float) * (size_t)n_conv * C;
 }
 
-hipError_t launch_resblock_bf16x3(int C, int waves_n, int kt, const RbParams& p, int batch,
-                                  hipStream_t stream, const char** name) {
+hipError_t launch_resblock_bf16x3(int C, int waves_n, int kt, int np, const RbParams& p,
+                                  int batch, hipStream_t stream, const char** name) {
   const int wm = C / 32;
   EntryRb* e = nullptr;
   for (auto& cand : g_entriesRb)
-    if (cand.kt == kt && cand.waves_m == wm && cand.waves_n == waves_n) e = &cand;
+    if (cand.kt == kt && cand.waves_m == wm && cand.waves_n == waves_n && cand.np == np) e = &cand;
   if (!e || C % 32 != 0) return hipErrorInvalidValue;
   const int nwin = kRbColsPerWave * waves_n;
   if (p.n_conv < 2 || p.n_conv > kRbMaxConv || (p.n_conv & 1)) return hipErrorInvalidValue;
@@ -327,8 +331,8 @@ hipError_t launch_resblock_bf16x3(int C, int waves_n, int kt, const RbParams& p,
   for (int i = 0; i < p.n_conv; ++i)
     if (p.dil[i] < 1 || (kt - 1) / 2 * p.dil[i] > rb_marg(C, waves_n)) return hipErrorInvalidValue;
   if (!e->name[0])
-    snprintf(e->name, sizeof(e->name), "resblock_bf16x3<%d, %d, %d>", e->kt, e->waves_m,
-             e->waves_n);
+    snprintf(e->name, sizeof(e->name), "resblock_bf16x3<%d, %d, %d, %d>", e->kt, e->waves_m,
+             e->waves_n, e->np);
   const size_t lds = rb_lds_bytes(C, waves_n, p.n_conv);
   if (lds > 160 * 1024) return hipErrorInvalidValue;
   if (!e->attr) {

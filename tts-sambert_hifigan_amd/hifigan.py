@@ -259,9 +259,12 @@ class HiFiGANGenerator(_HipWeights):
         self.set_precision(precision)
 
     def set_precision(self, precision: str):
-        """"fp32" (exact fp32 MFMA, default) or "bf16x3" (fp32 operands split into
+        """"fp32" (exact fp32 MFMA, default), "bf16x3" (fp32 operands split into
         two bf16 halves on the bf16 matrix cores; within ~1e-5 of the reference at
-        default weight scale).  Applies to the MRF / ResBlock submodules too."""
+        default weight scale) or "bf16w" (conv weights stored as bf16 — rounded when
+        committed to the handle, the module's own parameters untouched — activations
+        still split: the reference model with bf16-cast weights, to 1e-4).  Applies to
+        the MRF / ResBlock submodules too."""
         self._hfg_cfg = _lib.make_config(*self._hfg_args, precision=precision)
         for m in self.modules():
             if isinstance(m, _HipWeights):
