@@ -56,16 +56,38 @@ PEAK_HBM_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 PEAK_BF16_TFLOPS = 2500.0  # MI355X_MICROARCH.md: BF16 MFMA dense (no sparsity)
 
 
-def kernel_peak(name: str):
-    """(peak in algorithmic fp32-conv TFLOP/s, description) for one kernel."""
+def kernel_products(name: str) -> int:
+    """bf16 MFMA products per algorithmic multiply-add of a kernel (0: fp32 MFMA)."""
     if "bf16x3" in name or "mrf_thin_mfma" in name:
         # conv1d_bf16x3, resblock[16]_bf16x3, conv_ws_bf16x3, mrf_thin_mfma: 3 bf16 MFMA
         # products (hi*hi + hi*lo + lo*hi) per algorithmic multiply-add, 2 for the bf16w
         # instances (last template argument NP = 2: lo(w) = 0 skipped)
-        np_ = 2 if name.replace(" ", "").split("(")[0].endswith(",2>") else 3
+        return 2 if name.replace(" ", "").split("(")[0].endswith(",2>") else 3
+    return 0
+
+
+def kernel_peak(name: str):
+    """(peak in algorithmic fp32-conv TFLOP/s, description) for one kernel."""
+    np_ = kernel_products(name)
+    if np_:
         return (PEAK_BF16_TFLOPS / np_,
                 f"bf16 dense MFMA 2.5 PFLOP/s / {np_} split products")
     return PEAK_FP32_TFLOPS, "fp32 MFMA 157.3 TFLOP/s"
+
+
+def sustained_peak(pkg, dev_index, kind, cache={}):
+    """Live dense TFLOP/s and shader clock of a pure MFMA stream on this GPU
+    (hfg_probe_mfma_rate, csrc/probe.hip): kind 0 bf16 32x32x16, 1 fp32 32x32x2.
+    ~0.1 s of full-chip MFMA load after the timed region."""
+    if kind not in cache:
+        import ctypes
+        lib = pkg.load_library()
+        tf, mhz = ctypes.c_double(0.0), ctypes.c_double(0.0)
+        iters = 60000 if kind == 0 else 50000
+        rc = lib.hfg_probe_mfma_rate(int(dev_index), int(kind), iters, ctypes.byref(tf),
+                                     ctypes.byref(mhz))
+        cache[kind] = (tf.value, mhz.value) if rc == 0 else None
+    return cache[kind]
 
 
 def parse():
@@ -575,6 +597,19 @@ def main():
             "alg_bytes_per_launch": dom["bytes"] / dom["launches"],
             "share_of_step": dom["ms"] / args.steps / prof_ms.get(args.precision, ms_per_step),
         }
+        n_prod = kernel_products(dom_name)
+        sp = sustained_peak(pkg, dev_index, 0 if n_prod else 1)
+        if sp:
+            n_prod = max(n_prod, 1)
+            alg_peak = sp[0] / n_prod
+            line["roofline"]["peak_sustained"] = {
+                "mfma_dense_TFLOPs": sp[0], "clock_MHz": sp[1],
+                "algorithmic_TFLOPs": alg_peak, "frac": achieved / alg_peak,
+                "note": "pure MFMA stream on random operands, 2 blocks x 4 waves per CU, "
+                        "measured live after the timed region on this GPU (csrc/probe.hip, "
+                        f"hfg_probe_mfma_rate); divided by {n_prod} product(s) per "
+                        "multiply-add like 'peak'.  The DVFS ceiling a matrix kernel meets "
+                        "under full-chip load; 'peak' stays the datasheet figure"}
         if args.precision in prof_ms:
             line["roofline"]["pass"] = (
                 "per-kernel HIP-event times from a second timed pass of the same K steps on "

@@ -42,6 +42,17 @@ int hfg_forward_taps(hfg_handle* h, const float* mel, int64_t B, int64_t T, floa
                      int64_t out_len, void* workspace, size_t workspace_bytes,
                      float* const* taps, int n_taps, void* stream);
 
+/* Sustained matrix-core rate of GPU `device` under a full-chip load (csrc/probe.hip):
+ * 2 blocks x 4 waves per CU issue independent MFMAs back to back on random operands
+ * that change every instruction, `iters` rounds of 32 MFMAs per wave (after a warm-up
+ * launch of iters / 4).  kind 0: v_mfma_f32_32x32x16_bf16, kind 1:
+ * v_mfma_f32_32x32x2_f32, 4 independent accumulator chains per wave; kinds 2 / 3: the
+ * same with one chain (each MFMA accumulates onto the previous one's result; 8 MFMAs
+ * per round instead of 32).  *tflops <- dense TFLOP/s over the timed launch (HIP events),
+ * *mhz <- shader clock over it (s_memtime against the 100 MHz real-time counter).
+ * Measurement only (bench.py's roofline "peak_sustained"); synchronous. */
+int hfg_probe_mfma_rate(int device, int kind, int iters, double* tflops, double* mhz);
+
 #ifdef __cplusplus
 }
 #endif

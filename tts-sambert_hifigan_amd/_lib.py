@@ -13,7 +13,7 @@ from __future__ import annotations
 
 import ctypes
 import os
-from ctypes import (POINTER, c_char_p, c_int, c_int32, c_int64, c_size_t, c_void_p,
+from ctypes import (POINTER, c_char_p, c_double, c_int, c_int32, c_int64, c_size_t, c_void_p,
                     c_float)
 
 import torch  # noqa: F401  (see module docstring: bind torch's HIP runtime first)
@@ -172,6 +172,7 @@ SIGNATURES = {
     "hfg_checksum32": (c_int, [POINTER(c_void_p), POINTER(c_int64), c_int, c_void_p, c_void_p]),
     "hfg_forward_taps": (c_int, [c_void_p, c_void_p, c_int64, c_int64, c_void_p, c_int64,
                                  c_void_p, c_size_t, POINTER(c_void_p), c_int, c_void_p]),
+    "hfg_probe_mfma_rate": (c_int, [c_int, c_int, c_int, POINTER(c_double), POINTER(c_double)]),
     "hfg_mel_last_error": (c_char_p, []),
     "hfg_mel_create": (c_int, [POINTER(HfgMelConfig), c_int, POINTER(c_void_p)]),
     "hfg_mel_destroy": (None, [c_void_p]),

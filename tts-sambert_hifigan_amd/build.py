@@ -15,7 +15,7 @@ LIB_NAME = "libhifigan_hip.so"
 LIB_PATH = os.path.join(PKG_DIR, LIB_NAME)
 SOURCES = ["conv_kernels.hip", "conv_bf16x3.hip", "conv16_bf16x3.hip", "resblock_bf16x3.hip",
            "resblock16_bf16x3.hip", "mrf_thin.hip", "mrf_thin_mfma.hip",
-           "conv_ws_bf16x3.hip", "hifigan_capi.cpp", "mel_kernels.hip", "mel_capi.cpp"]
+           "conv_ws_bf16x3.hip", "probe.hip", "hifigan_capi.cpp", "mel_kernels.hip", "mel_capi.cpp"]
 HEADERS = ["kernels.h", "mel_kernels.h", "epilogue.h", "bf16x3_common.h", os.path.join("..", "..", "include", "hifigan_hip.h"),
            os.path.join("..", "..", "include", "hifigan_hip_inspect.h")]
 
