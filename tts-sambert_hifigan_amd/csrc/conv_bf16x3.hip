@@ -309,6 +309,11 @@ conv1d_bf16x3(const ConvParams p) {
     constexpr int XG = NTG >= 2 ? NTG - 2 : 0;
     using I6 = std::integral_constant<int, 6>;
     using I3 = std::integral_constant<int, 3>;
+    using I0 = std::integral_constant<int, 0>;
+    // every other tap stream pinned too: the next column tile's B reads issue after the
+    // current tile's first MFMA, not after its last (the default schedule waits on them
+    // right before use: one exposed LDS round trip per column tile)
+    constexpr bool p_pin = true;
     using T_ = std::true_type;
     using F_ = std::false_type;
     const int NG = p.n_chunks / NTG;
@@ -344,11 +349,15 @@ conv1d_bf16x3(const ConvParams p) {
           issue_next_w();
           if (ISX) load_x(gn);
           tap_stream(Ws, Xh, 0, tap0);
+          if constexpr (p_pin) pin_stream(I0{}, F_{}, F_{});
           if (STX) store_x(Xn);
         }
 #pragma unroll
         for (int jj = 1; jj < TPC; ++jj)
-          if (jj < nt) tap_stream(Ws, Xh, jj, tap0 + jj);
+          if (jj < nt) {
+            tap_stream(Ws, Xh, jj, tap0 + jj);
+            if constexpr (p_pin) pin_stream(I0{}, F_{}, F_{});
+          }
         // the slab of chunk c+1 must have landed; younger: this chunk's input loads
         if (ISX && !STX) wait_x(std::integral_constant<int, NX>{});
         else wait_vm<0>();
