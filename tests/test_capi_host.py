@@ -206,14 +206,15 @@ def bf2f(u16):
     return (u16.astype(np.uint32) << 16).view(np.float32)
 
 
-@pytest.mark.parametrize("big_tile", ["0", "3", "4", "c16"])
+@pytest.mark.parametrize("big_tile", ["0", "3", "4", "c16", "areg"])
 @pytest.mark.parametrize("preset", ["v1", "v2star"])
 def test_bf16x3_packing(pkg, preset, big_tile, monkeypatch):
     """bf16x3 layers: the packed hi/lo planes reconstruct every weight to ~2^-16
     relative, in the fragment order of conv_bf16x3.hip (every tile for M >= 128), of
     conv_ws_bf16x3.hip (4) and of conv16_bf16x3.hip (c16)."""
     monkeypatch.setenv("HFG_C16", "1" if big_tile == "c16" else "0")
-    monkeypatch.setenv("HFG_BF16X3_BIGTILE", "3" if big_tile == "c16" else big_tile)
+    monkeypatch.setenv("HFG_AREG", "1" if big_tile == "areg" else "0")
+    monkeypatch.setenv("HFG_BF16X3_BIGTILE", "3" if big_tile in ("c16", "areg") else big_tile)
     cfg = C.PRESETS[preset]
     sd = C.make_state_dict(cfg, seed=31)
     h = host_handle(pkg, cfg, "bf16x3")
@@ -221,7 +222,7 @@ def test_bf16x3_packing(pkg, preset, big_tile, monkeypatch):
         h.set_weight(k, torch.from_numpy(v))
     h.commit()
     # tile -> (WAVES_M, WM, TPC); ids 8 / 9 are conv_ws_bf16x3 / conv16_bf16x3 (kernels.h)
-    WAVES = {0: (2, 2, 4), 1: (1, 2, 2), 2: (1, 1, 4), 3: (2, 2, 2), 4: (2, 1, 4)}
+    WAVES = {0: (2, 2, 4), 1: (1, 2, 2), 2: (1, 1, 4), 3: (2, 2, 2), 4: (2, 1, 4), 5: (2, 2, 2)}
     n_checked = 0
     for mod in ["conv_pre", "mrfs.0.resblocks.2.convs1.1", "mrfs.1.resblocks.0.convs2.1",
                 "mrfs.2.resblocks.1.convs1.0", "mrfs.3.resblocks.2.convs2.1"]:
@@ -516,7 +517,7 @@ def test_bf16w_packing(pkg, preset, big_tile, monkeypatch):
             assert info["tile"] not in (8, 9), mod
             n_split += 1
             u = packed.view(np.uint16)
-            TPC = {0: 4, 1: 2, 2: 4, 3: 2, 4: 4}[info["tile"]]
+            TPC = {0: 4, 1: 2, 2: 4, 3: 2, 4: 4, 5: 2}[info["tile"]]
             planes = u.reshape(-1, TPC, 2, u.size // (info["m_tiles"] * info["n_chunks"] * TPC * 2))
             assert not planes[:, :, 1].any(), f"{mod}: lo plane not zero"
             hi = np.sort(bf2f(planes[:, :, 0]).ravel())

@@ -137,3 +137,21 @@ def test_lds_staged_epilogue_is_bitwise_invisible(pkg, dev, precision):
         torch.cuda.synchronize()
     assert torch.equal(outs["0"], outs["1"])
 
+
+
+@pytest.mark.parametrize("preset,B,T", [("v1", 2, 200), ("v1", 1, 96), ("v2star", 2, 64)])
+def test_areg_tile_is_bitwise_invisible(pkg, dev, preset, B, T):
+    """HFG_AREG=1: tile-3 layer convs on tile 5 (A fragments from global into registers,
+    one barrier per channel group; kernels.h) — the same MFMA sequence per output
+    element, so the wav is bitwise unchanged."""
+    from oracle import config as C
+    cfg = C.PRESETS[preset]
+    sd = C.make_state_dict(cfg, seed=36)
+    mel = torch.randn(B, 80, T, generator=torch.Generator().manual_seed(11))
+    outs = {}
+    for mode in ("0", "1"):
+        gen = _gen(pkg, cfg, sd, dev, "bf16x3", {"HFG_AREG": mode, "HFG_SMALL_TILE": "0"})
+        with torch.no_grad():
+            outs[mode] = gen(mel.to(dev), lengths=[T - 7 * b for b in range(B)])
+        torch.cuda.synchronize()
+    assert torch.equal(outs["0"], outs["1"])

@@ -29,6 +29,10 @@
 #include "epilogue.h"
 #include "kernels.h"
 
+#ifndef HFG_AREG_AD
+#define HFG_AREG_AD 1
+#endif
+
 namespace hfg {
 
 namespace {
@@ -36,9 +40,11 @@ typedef float floatx2 __attribute__((ext_vector_type(2)));
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 }  // namespace
 
-template <int KT_, int TPC, int WAVES_M, int WAVES_N, int WM, int WN, int WD, bool UPS, int NP>
+template <int KT_, int TPC, int WAVES_M, int WAVES_N, int WM, int WN, int WD, bool UPS, int NP,
+          bool AREG>
 __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N, 2)
 conv1d_bf16x3(const ConvParams p) {
+  static_assert(!AREG || (KT_ > 0 && !UPS && WM * WN >= 8), "AREG: compile-time taps, layer convs");
   constexpr int NW = WAVES_M * WAVES_N;
   constexpr int NT = 64 * NW;
   constexpr int MT = 32 * WM * WAVES_M;
@@ -64,7 +70,7 @@ conv1d_bf16x3(const ConvParams p) {
 
   extern __shared__ __attribute__((aligned(16))) __bf16 lds16[];
   __bf16* const Wbuf0 = lds16;
-  __bf16* const Xbuf0 = lds16 + WD * SLAB;
+  __bf16* const Xbuf0 = lds16 + (AREG ? 0 : WD * SLAB);
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -129,15 +135,21 @@ conv1d_bf16x3(const ConvParams p) {
   // it has 8 fewer input loads in flight than NX: every vmcnt wait that lets the input
   // loads stay outstanding counts them per wave (wait_x), or it would pass before the
   // older weight-slab DMA has landed
-  const bool x_short = XQ > 1 && (XQ - 1) * NT + wave_u * 64 >= 2 * XW;
+  // (AREG: no skip, and whole channel groups only (host-checked): the staging is
+  // straight-line code the tap schedule can interleave; the compiler counts its vmcnt)
+  const bool x_short = !AREG && XQ > 1 && (XQ - 1) * NT + wave_u * 64 >= 2 * XW;
   auto wait_x = [&](auto n_tag) {
     constexpr int N = decltype(n_tag)::value;
     static_assert(XQ == 1 || N >= 8, "vmcnt");
     if (x_short) wait_vm<(N >= 8 ? N - 8 : 0)>();
     else wait_vm<N>();
   };
+  // whole 32-bit range: an item holds up to 2^30 floats (4 GiB), and every offset the
+  // staging forms stays below that (byte offsets are unsigned 32-bit, as before)
+  const __amdgpu_buffer_rsrc_t xrs =
+      __builtin_amdgcn_make_buffer_rsrc((void*)xb, 0, -1, 0x00020000);
   auto load_x = [&](int g) {
-    const bool full = g * 16 + 16 <= p.C_in;  // block-uniform
+    const bool full = AREG || g * 16 + 16 <= p.C_in;  // block-uniform
     xok = 0;
 #pragma unroll
     for (int q = 0; q < XQ; ++q) {
@@ -156,10 +168,20 @@ conv1d_bf16x3(const ConvParams p) {
       const int ecap = full ? 7 : min(p.C_in - 1 - cb, 7);
       const uint32_t m8 = tok ? (ecap >= 7 ? 0xffu : (ecap < 0 ? 0u : (1u << (ecap + 1)) - 1u)) : 0u;
       xok |= m8 << (q * 8);
+      if (full) {
+        // whole group: buffer loads with the channel step in the scalar offset (one offset
+        // VGPR per row instead of eight); a lane outside the window reads channel e at
+        // t = 0 of its item (valid memory, masked by xok)
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const unsigned oe = o0 + (unsigned)(full ? e : max(min(e, ecap), 0)) * step;
-        xv[q][e] = *reinterpret_cast<const float*>(reinterpret_cast<const char*>(xb) + oe);
+        for (int e = 0; e < 8; ++e)
+          xv[q][e] = __builtin_bit_cast(
+              float, __builtin_amdgcn_raw_buffer_load_b32(xrs, (int)o0, e * xcs * 4, 0));
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const unsigned oe = o0 + (unsigned)max(min(e, ecap), 0) * step;
+          xv[q][e] = *reinterpret_cast<const float*>(reinterpret_cast<const char*>(xb) + oe);
+        }
       }
     }
   };
@@ -288,14 +310,131 @@ conv1d_bf16x3(const ConvParams p) {
 
   // ---- prologue: weight slabs of chunks 0..WD-2, input window of channel group 0 ----
   load_x(0);
+  if constexpr (!AREG) {
 #pragma unroll
-  for (int c = 0; c < WD - 1; ++c)
-    if (c < p.n_chunks) issue_w(c, Wbuf0 + c * SLAB);
+    for (int c = 0; c < WD - 1; ++c)
+      if (c < p.n_chunks) issue_w(c, Wbuf0 + c * SLAB);
+  }
   store_x(Xbuf0);
   wait_vm<0>();
   lds_barrier();
 
-  if constexpr (KT_ > 0 && WM * WN >= 8) {
+  if constexpr (AREG) {
+    // ---- A fragments from global into registers, AD taps ahead; one barrier per
+    // channel group.  Every wave reads its own (wave_m) rows of the packed slab stream
+    // (L2-resident; tile 3's packing) -- the two wave_n waves read the same rows -- so
+    // the weights need no LDS and no cross-wave handoff.  The input window is
+    // double-buffered per channel group as in the LDS-slab path: group g+1's loads issue
+    // at tap XT, land in the idle buffer at the group's last tap, and the barrier ending
+    // group g makes them visible (and frees the buffer group g read).  Per output element
+    // the MFMA sequence is the LDS-slab path's (channel groups x taps in order; lo*hi,
+    // hi*lo, hi*hi), so the result is bitwise the same.
+    constexpr int KT = KT_;
+    constexpr int NTG = (KT + TPC - 1) / TPC;
+    constexpr int AD = HFG_AREG_AD;           // A prefetch distance in taps (1 or 2)
+    constexpr int XT = KT >= 4 ? KT - 4 : 0;  // tap issuing the next group's input loads
+    static_assert(AD <= KT && XT < KT - 1, "AREG schedule");
+    using I0 = std::integral_constant<int, 0>;
+    using I2 = std::integral_constant<int, 2>;
+    using I6 = std::integral_constant<int, 6>;
+    using T_ = std::true_type;
+    using F_ = std::false_type;
+    const int NG = p.n_chunks / NTG;
+    const int wm_u = wave_u % WAVES_M;
+    // buffer loads: SGPR descriptor over this m-tile's stream + scalar tap offset + the
+    // lane's 16 B (no 64-bit address VGPRs per tap)
+    const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)wsrc, 0, (int)((int64_t)p.n_chunks * SLAB * 2), 0x00020000);
+    const int a_lane = lane * 16;
+    typedef bf16x8 ASet[2][WM];
+    ASet a0, a1, a2;
+    (void)a2;
+    auto load_a = [&](ASet& d, int g, int t) {
+      const int so = ((g * NTG + t / TPC) * SLAB + (t % TPC) * TAP_ELEMS + wm_u * WM * 512) * 2;
+#pragma unroll
+      for (int pl = 0; pl < 2; ++pl)
+#pragma unroll
+        for (int i = 0; i < WM; ++i)
+          d[pl][i] = __builtin_bit_cast(
+              bf16x8, __builtin_amdgcn_raw_buffer_load_b128(
+                          wrs, a_lane + (pl * WAVES_M * WM + i) * 1024, so, 0));
+    };
+    auto tap_regs = [&](const ASet& a, const __bf16* Xh, int tap) {
+      const __bf16* Xl = Xh + xplane;
+      bf16x8 bh[2], bl[2];
+      auto ldb = [&](int k) {
+        const int t = wave_n * 32 * WN + k * 32 + col + tap * p.dil;
+        const int off = t * XROW + 8 * (half ^ ((t >> 3) & 1));
+        bh[k & 1] = *reinterpret_cast<const bf16x8*>(Xh + off);
+        bl[k & 1] = *reinterpret_cast<const bf16x8*>(Xl + off);
+      };
+      ldb(0);
+#pragma unroll
+      for (int k = 0; k < WN; ++k) {
+        if (k + 1 < WN) ldb(k + 1);
+#pragma unroll
+        for (int i = 0; i < WM; ++i) {
+          if constexpr (NP == 3)
+            acc[i][k] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1][i], bh[k & 1], acc[i][k], 0, 0, 0);
+          acc[i][k] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][i], bl[k & 1], acc[i][k], 0, 0, 0);
+          acc[i][k] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][i], bh[k & 1], acc[i][k], 0, 0, 0);
+        }
+      }
+    };
+    // one tap's interleave: B(0) first, then per MFMA up to NV VALU and (LD) one global
+    // load, the next B pair after each column tile's first MFMA, a DS write every 4th
+    // MFMA (ST)
+    auto pin_regs = [&](auto nv_tag, auto ld_tag, auto st_tag) {
+      constexpr int NV = decltype(nv_tag)::value;
+      constexpr bool LD = decltype(ld_tag)::value, ST = decltype(st_tag)::value;
+      __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+#pragma unroll
+      for (int s = 0; s < NP * WM * WN; ++s) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x002, NV, 0);
+        if (LD) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+        if (ST && s % 4 == 3) __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);
+        if (s % (NP * WM) == 0 && s / (NP * WM) + 1 < WN)
+          __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    };
+    load_a(a0, 0, 0);
+    if constexpr (AD == 2) load_a(a1, 0, 1);
+    for (int g = 0; g < NG; ++g) {
+      const __bf16* Xh = Xbuf0 + (g & 1) * xbuf;
+      __bf16* const Xn = Xbuf0 + ((g + 1) & 1) * xbuf;
+      const int gn = min(g + 1, NG - 1);
+#pragma unroll
+      for (int t = 0; t < KT; ++t) {
+        // A of tap t + AD: the next group's first taps near the end (past the last group
+        // a harmless re-read of its own)
+        ASet& an = AD == 2 ? a2 : a1;
+        if (t + AD < KT) load_a(an, g, t + AD);
+        else load_a(an, gn, t + AD - KT);
+        if (t == XT) {
+          load_x(gn);
+          tap_regs(a0, Xh, t);
+          pin_regs(I0{}, T_{}, F_{});
+        } else if (t == KT - 1) {
+          store_x(Xn);
+          tap_regs(a0, Xh, t);
+          pin_regs(I6{}, T_{}, T_{});
+        } else {
+          tap_regs(a0, Xh, t);
+          pin_regs(I2{}, T_{}, F_{});
+        }
+#pragma unroll
+        for (int pl = 0; pl < 2; ++pl)
+#pragma unroll
+          for (int i = 0; i < WM; ++i) {
+            a0[pl][i] = a1[pl][i];
+            if constexpr (AD == 2) a1[pl][i] = a2[pl][i];
+          }
+      }
+      lds_barrier();
+    }
+  } else if constexpr (KT_ > 0 && WM * WN >= 8) {
     // ---- 64x128-per-wave tile, compile-time taps: the chunk loop unrolled over one
     // channel group, so the chunks that stage the next input window are their own
     // straight-line code.  That staging (the loads, or the conversion and LDS store)
@@ -538,7 +677,7 @@ template <int KT, int TILE, bool UPS, int NP>
 struct Inst3 {
   static constexpr Bf16x3Cfg t = kBf16x3Tiles[TILE];
   static ConvFn3 fn() {
-    return conv1d_bf16x3<KT, t.TPC, t.WAVES_M, t.WAVES_N, t.WM, t.WN, t.WD, UPS, NP>;
+    return conv1d_bf16x3<KT, t.TPC, t.WAVES_M, t.WAVES_N, t.WM, t.WN, t.WD, UPS, NP, t.AREG != 0>;
   }
 };
 
@@ -561,16 +700,20 @@ struct Entry3 {
 
 // NP 3: hi*hi + hi*lo + lo*hi (bf16x3); NP 2: hi*hi + hi*lo for bf16-valued weights
 // (HFG_DTYPE_BF16W: the weights' lo plane is zero), tiles 1-4
+// tile 5 (AREG): compile-time taps, layer convs only
+#define HFG3_AREG(KT) HFG3_ENTRY(KT, 5, false, 3), HFG3_ENTRY(KT, 5, false, 2)
 Entry3 g_entries3[] = {
     HFG3_TILES(3, false), HFG3_TILES(5, false), HFG3_TILES(7, false), HFG3_TILES(11, false),
     HFG3_TILES(0, false), HFG3_TILES(2, true),  HFG3_TILES(0, true),
+    HFG3_AREG(3),         HFG3_AREG(5),         HFG3_AREG(7),         HFG3_AREG(11),
 };
 
 }  // namespace
 
 size_t bf16x3_lds_bytes(int tile, int kt, int dil) {
   const Bf16x3Cfg& t = kBf16x3Tiles[tile];
-  const size_t slab = (size_t)t.TPC * 2 * t.MT() * 16;  // bf16: taps x planes x rows x 16 ch
+  // bf16: taps x planes x rows x 16 ch (no slab ring on the AREG tile)
+  const size_t slab = t.AREG ? 0 : (size_t)t.TPC * 2 * t.MT() * 16;
   const int xw = t.NTILE() + (kt - 1) * dil;
   const size_t xplane = ((size_t)xw * 16 + 7) & ~(size_t)7;
   return sizeof(__bf16) * (t.WD * slab + 2 * 2 * xplane);  // weight ring + 2 (hi,lo) windows
@@ -592,9 +735,9 @@ hipError_t launch_conv_bf16x3(int tile, int kt, bool ups, int np, const ConvPara
     return hipErrorInvalidValue;
   const Bf16x3Cfg& t = kBf16x3Tiles[tile];
   if (!e->name[0])
-    snprintf(e->name, sizeof(e->name), "conv1d_bf16x3<%d, %d, %d, %d, %d, %d, %d, %s, %d>",
+    snprintf(e->name, sizeof(e->name), "conv1d_bf16x3<%d, %d, %d, %d, %d, %d, %d, %s, %d%s>",
              e->kt, t.TPC, t.WAVES_M, t.WAVES_N, t.WM, t.WN, t.WD, e->ups ? "true" : "false",
-             e->np);
+             e->np, t.AREG ? ", true" : "");
   size_t lds = bf16x3_lds_bytes(tile, kt, p.dil);
   if (p.epi_lds && !ups)
     lds = std::max(lds, (size_t)t.threads() / 64 * 32 * (32 * t.WN + 8) * sizeof(float));

@@ -143,6 +143,7 @@ struct hfg_handle {
   bool mfma16 = true;        // 16x16x32-shape ResBlock kernel for C = 32 (HFG_MFMA16=0: off)
   int ups_swizzle = 1;       // XCD swizzle of the upsampler blocks (HFG_UPS_SWIZZLE=0: off)
   int np = 3;                // MFMA products per multiply-add: 3 (bf16x3), 2 (bf16w: lo(w) = 0)
+  int areg = 1;              // tile-3 layer convs on tile 5 (A in registers; HFG_AREG=0: off)
   int epi_lds = 1;           // LDS-staged float4 epilogue of the bf16x3 layer convs (HFG_EPI_LDS=0: off)
   int small_tile = -1;       // small-grid tile: -1 auto (grid < kSmallGridBlocks), 0 never,
                              // 1 always (HFG_SMALL_TILE)
@@ -352,6 +353,11 @@ int build_layers(hfg_handle* h) {
         hfg::bf16x3_tile_for_rows(L.M) >= 0 && hfg::bf16x3_supported(L.KT, L.dil)) {
       // split-precision path: chunk = 16 channels x TPC taps
       L.tile = hfg::bf16x3_tile_for_rows(L.M, h->big_tile == hfg::kWsTile ? 3 : h->big_tile);
+      // tile 3 with the A fragments in registers (same packing): layer convs whose tap
+      // count has a compile-time instance, whole 16-channel groups
+      if (h->areg && L.tile == 3 && L.kind == L_CONV && L.C_in % 16 == 0 &&
+          (L.KT == 3 || L.KT == 5 || L.KT == 7 || L.KT == 11))
+        L.tile = hfg::kAregTile;
       const hfg::Bf16x3Cfg& t3 = hfg::kBf16x3Tiles[L.tile];
       L.prec = 1;
       L.CK = hfg::kBf16x3Ck;
@@ -1495,6 +1501,7 @@ int create_impl(const hfg_config* cfg, bool mrf_only, int device, hfg_handle** o
   if (const char* rc = getenv("HFG_RB_CONC")) h->rb_conc = atoi(rc);
   if (const char* us = getenv("HFG_UPS_SWIZZLE")) h->ups_swizzle = atoi(us);
   if (const char* el = getenv("HFG_EPI_LDS")) h->epi_lds = atoi(el);
+  if (const char* ar = getenv("HFG_AREG")) h->areg = atoi(ar) != 0;
   if (const char* ce = getenv("HFG_C16")) h->c16 = atoi(ce) != 0;
   if (const char* se = getenv("HFG_SPLIT")) h->split = atoi(se);
   if (const char* rn = getenv("HFG_RB64_NARROW")) h->rb64_narrow = atoi(rn) != 0;

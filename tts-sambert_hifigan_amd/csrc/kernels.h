@@ -94,11 +94,12 @@ constexpr int halo_max(int dkt) { return dkt == 0 ? 192 : (dkt - 1) * kMaxDil; }
 // WD = depth of the weight-slab ring (chunks in flight: WD - 1).
 struct Bf16x3Cfg {
   int WAVES_M, WAVES_N, WM, WN, TPC, WD;
+  int AREG;  // 1: A fragments loaded from global straight into registers (no LDS ring)
   constexpr int MT() const { return 32 * WM * WAVES_M; }
   constexpr int NTILE() const { return 32 * WN * WAVES_N; }
   constexpr int threads() const { return 64 * WAVES_M * WAVES_N; }
 };
-constexpr int kBf16x3Tiles_n = 5;
+constexpr int kBf16x3Tiles_n = 6;
 // 0: 128x256, 2x4 waves of 64x64, 4 taps/chunk, 3-deep weight ring (1 block/CU)
 // 1: 64x256, 1x4 waves of 64x64, 2 taps/chunk (2 blocks/CU)
 // 2: 32x256, 1x4 waves of 32x64, 4 taps/chunk (2 blocks/CU)
@@ -108,9 +109,14 @@ constexpr int kBf16x3Tiles_n = 5;
 //    tile-3 grid would leave most CUs idle (small batches, short utterances) runs on it
 //    instead; every output element sees the same MFMA sequence (channel groups x taps in
 //    order, lo*hi, hi*lo, hi*hi) on either tile, so the choice is bitwise invisible.
+// 5: tile 3's geometry and packing with the A fragments read by each wave from global
+//    (L2) into registers two taps ahead instead of through an LDS slab ring: LDS holds
+//    only the input windows, and the block synchronises once per channel group instead
+//    of once per 2-tap chunk (layer convs with compile-time taps; HFG_AREG)
 constexpr Bf16x3Cfg kBf16x3Tiles[kBf16x3Tiles_n] = {
-    {2, 4, 2, 2, 4, 3}, {1, 4, 2, 2, 2, 2}, {1, 4, 1, 2, 4, 2}, {2, 2, 2, 4, 2, 2},
-    {2, 1, 1, 2, 4, 2}};
+    {2, 4, 2, 2, 4, 3, 0}, {1, 4, 2, 2, 2, 2, 0}, {1, 4, 1, 2, 4, 2, 0}, {2, 2, 2, 4, 2, 2, 0},
+    {2, 1, 1, 2, 4, 2, 0}, {2, 2, 2, 4, 2, 2, 1}};
+constexpr int kAregTile = 5;
 constexpr int kBf16x3SmallTile = 4;
 // a layer launch runs on the small tile when its tile-3 grid has fewer blocks than this
 // (tile 3 fits 2 blocks per CU: 512 slots on 256 CUs)
