@@ -65,7 +65,12 @@ conv1d_bf16x3(const ConvParams p) {
   const int n_tg = (KT + TPC - 1) / TPC;          // tap groups per channel group
   // one staged input window per 16-channel group serves all KT taps
   const int XW = NTILE + (KT - 1) * p.dil;
-  const int xplane = (XW * XROW + 7) & ~7;        // bf16 per X plane
+  // AREG: the planes hold a row for every staging task (XQ*NT/2 >= XW_MAX rows), so
+  // store_x writes all its tasks unconditionally (rows >= XW are never read) and stays
+  // straight-line code the tap schedule interleaves into the MFMA stream
+  constexpr int XROWS_AREG = XQ * NT / 2;
+  static_assert(XROWS_AREG >= XW_MAX, "AREG planes");
+  const int xplane = AREG ? XROWS_AREG * XROW : (XW * XROW + 7) & ~7;  // bf16 per X plane
   const int xbuf = 2 * xplane;                    // hi + lo planes
 
   extern __shared__ __attribute__((aligned(16))) __bf16 lds16[];
@@ -130,6 +135,12 @@ conv1d_bf16x3(const ConvParams p) {
   // time from a bit mask, so the loads' latency hides behind the chunk's MFMAs
   float xv[XQ][8];
   uint32_t xok = 0;
+  // AREG (whole groups: one in-window flag per task row): the zero padding and the
+  // pre-activation as max(v*s1, v*s2) with per-row factors (s1, s2) = (1, slope) inside
+  // the window (slope 1 without act_in: v) and (0, 0) outside (+-0): bitwise lrelu3(v) or
+  // v or 0, in 3 VALU ops and no canonicalising max on the loaded value
+  float xs1[XQ], xs2[XQ];
+  const float slope = p.act_in ? kLReluSlope : 1.0f;
   const int wave_u = __builtin_amdgcn_readfirstlane(wave);
   // a wave with no task in the (mostly idle) last staging row skips that row's loads, so
   // it has 8 fewer input loads in flight than NX: every vmcnt wait that lets the input
@@ -168,6 +179,8 @@ conv1d_bf16x3(const ConvParams p) {
       const int ecap = full ? 7 : min(p.C_in - 1 - cb, 7);
       const uint32_t m8 = tok ? (ecap >= 7 ? 0xffu : (ecap < 0 ? 0u : (1u << (ecap + 1)) - 1u)) : 0u;
       xok |= m8 << (q * 8);
+      xs1[q] = tok ? 1.0f : 0.0f;
+      xs2[q] = tok ? slope : 0.0f;
       if (full) {
         // whole group: buffer loads with the channel step in the scalar offset (one offset
         // VGPR per row instead of eight); a lane outside the window reads channel e at
@@ -190,16 +203,21 @@ conv1d_bf16x3(const ConvParams p) {
 #pragma unroll
     for (int q = 0; q < XQ; ++q) {
       const int i = tid + q * NT;
-      if (i < 2 * XW) {
+      if (AREG || i < 2 * XW) {
         bf16x8 h, l;
 #pragma unroll
         for (int e = 0; e < 8; e += 2) {
           floatx2 a;
-          a[0] = (xok >> (q * 8 + e)) & 1u ? xv[q][e] : 0.f;
-          a[1] = (xok >> (q * 8 + e + 1)) & 1u ? xv[q][e + 1] : 0.f;
-          if (p.act_in) {
-            a[0] = lrelu3(a[0]);
-            a[1] = lrelu3(a[1]);
+          if constexpr (AREG) {
+            a[0] = fmaxf(xv[q][e] * xs1[q], xv[q][e] * xs2[q]);
+            a[1] = fmaxf(xv[q][e + 1] * xs1[q], xv[q][e + 1] * xs2[q]);
+          } else {
+            a[0] = (xok >> (q * 8 + e)) & 1u ? xv[q][e] : 0.f;
+            a[1] = (xok >> (q * 8 + e + 1)) & 1u ? xv[q][e + 1] : 0.f;
+            if (p.act_in) {
+              a[0] = lrelu3(a[0]);
+              a[1] = lrelu3(a[1]);
+            }
           }
           const bf16x2 hh = __builtin_convertvector(a, bf16x2);
           const floatx2 hf = __builtin_convertvector(hh, floatx2);
@@ -210,7 +228,12 @@ conv1d_bf16x3(const ConvParams p) {
           l[e + 1] = ll[1];
         }
         const int t = i >> 1;
-        const int off = t * XROW + 8 * ((i & 1) ^ ((t >> 3) & 1));  // swizzled half
+        // AREG: the two 8-channel halves in planes of their own (16-B rows: a half-wave's
+        // 32 consecutive rows are one conflict-free 512-B run for any tap shift, so a tap
+        // is one address add and the reads take immediate offsets); else one 32-B row per
+        // t with the 16-B halves XOR-swizzled
+        const int off = AREG ? (i & 1) * XROWS_AREG * 8 + t * 8
+                             : t * XROW + 8 * ((i & 1) ^ ((t >> 3) & 1));
         *reinterpret_cast<bf16x8*>(Xh + off) = h;
         *reinterpret_cast<bf16x8*>(Xl + off) = l;
       }
@@ -363,8 +386,8 @@ conv1d_bf16x3(const ConvParams p) {
       const __bf16* Xl = Xh + xplane;
       bf16x8 bh[2], bl[2];
       auto ldb = [&](int k) {
-        const int t = wave_n * 32 * WN + k * 32 + col + tap * p.dil;
-        const int off = t * XROW + 8 * (half ^ ((t >> 3) & 1));
+        const int off = half * XROWS_AREG * 8 + (wave_n * 32 * WN + col) * 8 + k * 32 * 8 +
+                        tap * p.dil * 8;
         bh[k & 1] = *reinterpret_cast<const bf16x8*>(Xh + off);
         bl[k & 1] = *reinterpret_cast<const bf16x8*>(Xl + off);
       };
@@ -714,7 +737,8 @@ size_t bf16x3_lds_bytes(int tile, int kt, int dil) {
   const Bf16x3Cfg& t = kBf16x3Tiles[tile];
   // bf16: taps x planes x rows x 16 ch (no slab ring on the AREG tile)
   const size_t slab = t.AREG ? 0 : (size_t)t.TPC * 2 * t.MT() * 16;
-  const int xw = t.NTILE() + (kt - 1) * dil;
+  // AREG: a plane row per staging task (the kernel's XROWS_AREG)
+  const int xw = t.AREG ? bf16x3_areg_rows(kt, t) : t.NTILE() + (kt - 1) * dil;
   const size_t xplane = ((size_t)xw * 16 + 7) & ~(size_t)7;
   return sizeof(__bf16) * (t.WD * slab + 2 * 2 * xplane);  // weight ring + 2 (hi,lo) windows
 }

@@ -125,6 +125,14 @@ constexpr int kBf16x3Ck = 16;  // channels per chunk (one MFMA k-step per tap)
 // largest (KT-1)*dil window halo of the bf16x3 layer kernel (sizes its staging
 // registers: 3 tasks per thread for the 256-column tiles); wider layers run on the fp32 path
 constexpr int kBf16x3MaxHalo = 128;
+// rows of one staged input plane on the AREG tile: one per staging task (XQ * NT / 2),
+// as conv1d_bf16x3 computes XQ from the largest window of the instantiation
+constexpr int bf16x3_areg_rows(int kt, const Bf16x3Cfg& t) {
+  const int halo = (kt - 1) * kMaxDil < kBf16x3MaxHalo ? (kt - 1) * kMaxDil : kBf16x3MaxHalo;
+  const int xw_max = t.NTILE() + halo;
+  const int nt = t.threads();
+  return (2 * xw_max + nt - 1) / nt * nt / 2;
+}
 inline int bf16x3_tile_for_rows(int M, int big_tile = 0) {
   return M >= 128 ? big_tile : (M >= 64 ? 1 : (M >= 32 ? 2 : -1));
 }
