@@ -30,7 +30,7 @@
 #include "kernels.h"
 
 #ifndef HFG_AREG_AD
-#define HFG_AREG_AD 1
+#define HFG_AREG_AD 2
 #endif
 
 namespace hfg {
