@@ -1,5 +1,5 @@
 #!/bin/bash
-# AREG straight-line staging (half planes, folded pad/lrelu factors): parity first, then
+# tile-5 A/B runner: parity (latency-path, parity and property GPU tests), then a same-box A/B against
 # the HEAD build (profiles/ab_build.sh).  usage: bash profiles/r02_stage_ab.sh TAG
 set -o pipefail
 TAG=${1:-stg}

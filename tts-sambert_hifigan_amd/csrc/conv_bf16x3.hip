@@ -382,19 +382,23 @@ conv1d_bf16x3(const ConvParams p) {
               bf16x8, __builtin_amdgcn_raw_buffer_load_b128(
                           wrs, a_lane + (pl * WAVES_M * WM + i) * 1024, so, 0));
     };
-    auto tap_regs = [&](const ASet& a, const __bf16* Xh, int tap) {
-      const __bf16* Xl = Xh + xplane;
-      bf16x8 bh[2], bl[2];
-      auto ldb = [&](int k) {
-        const int off = half * XROWS_AREG * 8 + (wave_n * 32 * WN + col) * 8 + k * 32 * 8 +
-                        tap * p.dil * 8;
-        bh[k & 1] = *reinterpret_cast<const bf16x8*>(Xh + off);
-        bl[k & 1] = *reinterpret_cast<const bf16x8*>(Xl + off);
-      };
-      ldb(0);
+    // B fragments: a two-deep ring over the column tiles that carries across the taps of
+    // a channel group (the last tile of tap t reads tap t+1's first pair), so a tap's first
+    // MFMAs do not wait on an LDS round trip; only the first tap after the group barrier
+    // reads its first pair on the spot
+    bf16x8 bh[2], bl[2];
+    auto ldb = [&](const __bf16* Xh, int tap, int k) {
+      const int off = half * XROWS_AREG * 8 + (wave_n * 32 * WN + col) * 8 + (k % WN) * 32 * 8 +
+                      (tap + k / WN) * p.dil * 8;
+      bh[k & 1] = *reinterpret_cast<const bf16x8*>(Xh + off);
+      bl[k & 1] = *reinterpret_cast<const bf16x8*>(Xh + xplane + off);
+    };
+    static_assert(WN % 2 == 0, "B ring parity across taps");
+    auto tap_regs = [&](const ASet& a, const __bf16* Xh, int tap, bool pre_in, bool pre_out) {
+      if (!pre_in) ldb(Xh, tap, 0);
 #pragma unroll
       for (int k = 0; k < WN; ++k) {
-        if (k + 1 < WN) ldb(k + 1);
+        if (k + 1 < WN || pre_out) ldb(Xh, tap, k + 1);  // k + 1 == WN: tap + 1, tile 0
 #pragma unroll
         for (int i = 0; i < WM; ++i) {
           if constexpr (NP == 3)
@@ -404,20 +408,21 @@ conv1d_bf16x3(const ConvParams p) {
         }
       }
     };
-    // one tap's interleave: B(0) first, then per MFMA up to NV VALU and (LD) one global
-    // load, the next B pair after each column tile's first MFMA, a DS write every 4th
+    // one tap's interleave: B(0) first (unless the previous tap read it), then per MFMA up to
+    // NV VALU and (LD) one global load, the next B pair after each column tile's first MFMA
+    // (after the last tile's: the next tap's first pair when pre_out), a DS write every 4th
     // MFMA (ST)
-    auto pin_regs = [&](auto nv_tag, auto ld_tag, auto st_tag) {
+    auto pin_regs = [&](auto nv_tag, auto ld_tag, auto st_tag, bool pre_in, bool pre_out) {
       constexpr int NV = decltype(nv_tag)::value;
       constexpr bool LD = decltype(ld_tag)::value, ST = decltype(st_tag)::value;
-      __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+      if (!pre_in) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
 #pragma unroll
       for (int s = 0; s < NP * WM * WN; ++s) {
         __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
         __builtin_amdgcn_sched_group_barrier(0x002, NV, 0);
         if (LD) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
         if (ST && s % 4 == 3) __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);
-        if (s % (NP * WM) == 0 && s / (NP * WM) + 1 < WN)
+        if (s % (NP * WM) == 0 && (s / (NP * WM) + 1 < WN || pre_out))
           __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
       }
       __builtin_amdgcn_sched_barrier(0);
@@ -435,17 +440,18 @@ conv1d_bf16x3(const ConvParams p) {
         ASet& an = AD == 2 ? a2 : a1;
         if (t + AD < KT) load_a(an, g, t + AD);
         else load_a(an, gn, t + AD - KT);
+        const bool pre_in = t > 0, pre_out = t + 1 < KT;
         if (t == XT) {
           load_x(gn);
-          tap_regs(a0, Xh, t);
-          pin_regs(I0{}, T_{}, F_{});
+          tap_regs(a0, Xh, t, pre_in, pre_out);
+          pin_regs(I0{}, T_{}, F_{}, pre_in, pre_out);
         } else if (t == KT - 1) {
           store_x(Xn);
-          tap_regs(a0, Xh, t);
-          pin_regs(I6{}, T_{}, T_{});
+          tap_regs(a0, Xh, t, pre_in, pre_out);
+          pin_regs(I6{}, T_{}, T_{}, pre_in, pre_out);
         } else {
-          tap_regs(a0, Xh, t);
-          pin_regs(I2{}, T_{}, F_{});
+          tap_regs(a0, Xh, t, pre_in, pre_out);
+          pin_regs(I2{}, T_{}, F_{}, pre_in, pre_out);
         }
 #pragma unroll
         for (int pl = 0; pl < 2; ++pl)
