@@ -97,6 +97,12 @@ conv1d_bf16x3(const ConvParams p) {
     id /= ny;
     tx = id % nx;
     b = id / nx;
+    // the divisions expand to VALU code: without this the compiler treats the results as
+    // per-lane values, and every buffer load whose descriptor derives from b (the input
+    // staging) became a readfirstlane waterfall loop
+    mt = __builtin_amdgcn_readfirstlane(mt);
+    tx = __builtin_amdgcn_readfirstlane(tx);
+    b = __builtin_amdgcn_readfirstlane(b);
   }
   const int n0 = p.n_base + tx * NTILE;
   const int half = lane >> 5;
