@@ -139,6 +139,30 @@ def test_lds_staged_epilogue_is_bitwise_invisible(pkg, dev, precision):
 
 
 
+@pytest.mark.parametrize("precision", ["fp32", "bf16x3"])
+@pytest.mark.parametrize("preset", ["nonexact", "v1"])
+def test_ragged_batch_with_concurrent_resblocks_equals_solo(pkg, dev, preset, precision):
+    """A ragged batch whose stage lengths are not multiples of 4 (non-exact upsampling:
+    5T + 1) through the concurrent-ResBlock schedule (small grids) and its mrf_combine
+    launch: every item bitwise equal to the utterance run alone.  (mrf_combine once
+    skipped a whole 4-sample group on its first sample's column, losing the next channel
+    row's first samples.)"""
+    from oracle import config as C
+    cfg = C.PRESETS[preset]
+    sd = C.make_state_dict(cfg, seed=38)
+    mel = torch.randn(3, 80, 77, generator=torch.Generator().manual_seed(14))
+    lens = [77, 60, 33]
+    gen = _gen(pkg, cfg, sd, dev, precision, {"HFG_RB_CONC": "1"})
+    with torch.no_grad():
+        out = gen(mel.to(dev), lengths=lens)
+        for b, n in enumerate(lens):
+            solo = gen(mel[b:b + 1, :, :n].to(dev))
+            m = solo.shape[-1]
+            assert torch.equal(out[b:b + 1, :, :m], solo), (b, n)
+            assert not torch.any(out[b, :, m:]), (b, n)  # zero past the item's length
+    torch.cuda.synchronize()
+
+
 @pytest.mark.parametrize("preset,B,T", [("v1", 2, 200), ("v1", 1, 96), ("v2star", 2, 64)])
 def test_areg_tile_is_bitwise_invisible(pkg, dev, preset, B, T):
     """HFG_AREG=1: tile-3 layer convs on tile 5 (A fragments from global into registers,

@@ -70,7 +70,10 @@ conv1d_bf16x3(const ConvParams p) {
   // straight-line code the tap schedule interleaves into the MFMA stream
   constexpr int XROWS_AREG = XQ * NT / 2;
   static_assert(XROWS_AREG >= XW_MAX, "AREG planes");
-  const int xplane = AREG ? XROWS_AREG * XROW : (XW * XROW + 7) & ~7;  // bf16 per X plane
+  // AREG half planes (8 channels, 16-B rows) padded by 64 B: a ds_write_b128 lane group
+  // (8 lanes: 4 rows of each half) then covers the 32 write banks once
+  constexpr int HPS_AREG = XROWS_AREG * 8 + 32;
+  const int xplane = AREG ? 2 * HPS_AREG : (XW * XROW + 7) & ~7;  // bf16 per X plane
   const int xbuf = 2 * xplane;                    // hi + lo planes
 
   extern __shared__ __attribute__((aligned(16))) __bf16 lds16[];
@@ -238,7 +241,7 @@ conv1d_bf16x3(const ConvParams p) {
         // 32 consecutive rows are one conflict-free 512-B run for any tap shift, so a tap
         // is one address add and the reads take immediate offsets); else one 32-B row per
         // t with the 16-B halves XOR-swizzled
-        const int off = AREG ? (i & 1) * XROWS_AREG * 8 + t * 8
+        const int off = AREG ? (i & 1) * HPS_AREG + t * 8
                              : t * XROW + 8 * ((i & 1) ^ ((t >> 3) & 1));
         *reinterpret_cast<bf16x8*>(Xh + off) = h;
         *reinterpret_cast<bf16x8*>(Xl + off) = l;
@@ -394,7 +397,7 @@ conv1d_bf16x3(const ConvParams p) {
     // reads its first pair on the spot
     bf16x8 bh[2], bl[2];
     auto ldb = [&](const __bf16* Xh, int tap, int k) {
-      const int off = half * XROWS_AREG * 8 + (wave_n * 32 * WN + col) * 8 + (k % WN) * 32 * 8 +
+      const int off = half * HPS_AREG + (wave_n * 32 * WN + col) * 8 + (k % WN) * 32 * 8 +
                       (tap + k / WN) * p.dil * 8;
       bh[k & 1] = *reinterpret_cast<const bf16x8*>(Xh + off);
       bl[k & 1] = *reinterpret_cast<const bf16x8*>(Xh + xplane + off);
@@ -751,7 +754,8 @@ size_t bf16x3_lds_bytes(int tile, int kt, int dil) {
   const size_t slab = t.AREG ? 0 : (size_t)t.TPC * 2 * t.MT() * 16;
   // AREG: a plane row per staging task (the kernel's XROWS_AREG)
   const int xw = t.AREG ? bf16x3_areg_rows(kt, t) : t.NTILE() + (kt - 1) * dil;
-  const size_t xplane = ((size_t)xw * 16 + 7) & ~(size_t)7;
+  // AREG: two padded half planes (the kernel's HPS_AREG)
+  const size_t xplane = t.AREG ? (size_t)xw * 16 + 64 : ((size_t)xw * 16 + 7) & ~(size_t)7;
   return sizeof(__bf16) * (t.WD * slab + 2 * 2 * xplane);  // weight ring + 2 (hi,lo) windows
 }
 

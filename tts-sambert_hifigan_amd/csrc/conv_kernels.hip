@@ -427,8 +427,9 @@ __global__ void __launch_bounds__(256) mrf_combine_kernel(MrfCombineArgs a) {
   for (int64_t i = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4; i < n;
        i += (int64_t)gridDim.x * 256 * 4) {
     const int t = (int)(i % a.L);
-    if (t >= len_b) continue;
     if ((a.L & 3) == 0) {
+      // 4 samples of one channel row (L % 4 == 0): one test for the group
+      if (t >= len_b) continue;
       float4 acc = *reinterpret_cast<const float4*>(a.o[0] + base + i);
       for (int j = 1; j < a.n; ++j) {
         const float4 v = *reinterpret_cast<const float4*>(a.o[j] + base + i);
@@ -443,7 +444,11 @@ __global__ void __launch_bounds__(256) mrf_combine_kernel(MrfCombineArgs a) {
       acc.w = acc.w / a.div;
       *reinterpret_cast<float4*>(a.y + base + i) = acc;
     } else {
+      // a group of 4 can straddle two channel rows: each sample tests its own column
+      // (skipping the group on its first sample's column lost the next row's first
+      // samples of a ragged item)
       for (int e = 0; e < 4 && i + e < n; ++e) {
+        if ((t + e) % a.L >= len_b) continue;
         float acc = a.o[0][base + i + e];
         for (int j = 1; j < a.n; ++j) acc = acc + a.o[j][base + i + e];
         a.y[base + i + e] = acc / a.div;
