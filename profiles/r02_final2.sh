@@ -4,10 +4,11 @@
 set -o pipefail
 export TMPDIR=/tmp
 R=$GRAFT_REPO_ROOT
-mkdir -p $R/gpurun_out/f2
+T=${1:-f2}
+mkdir -p $R/gpurun_out/$T
 cd $R
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/f2/pytest.log 2>&1 &&
-timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/f2/smoke.log 2>&1 &&
-timeout -k 10 400 python bench.py > gpurun_out/f2/bench.json 2> gpurun_out/f2/bench.err &&
-bash profiles/run_rocprof.sh f2 &&
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/$T/pytest.log 2>&1 &&
+timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/$T/smoke.log 2>&1 &&
+timeout -k 10 400 python bench.py > gpurun_out/$T/bench.json 2> gpurun_out/$T/bench.err &&
+bash profiles/run_rocprof.sh $T &&
 bash profiles/r02_sq.sh
