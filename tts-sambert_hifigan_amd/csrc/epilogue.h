@@ -193,7 +193,10 @@ __device__ __forceinline__ void conv_epilogue_lds(const ConvParams& p, floatx16e
       for (int u = 0; u < 4; ++u) {
         float* dst = outb + (int64_t)row[u] * p.N + n[u];
         if (full[u]) {
-          *reinterpret_cast<float4*>(dst) = v[u];
+          // streamed once (the next launch reads it from HBM / MALL): non-temporal
+          typedef float f4v __attribute__((ext_vector_type(4)));
+          const f4v nv = {v[u].x, v[u].y, v[u].z, v[u].w};
+          __builtin_nontemporal_store(nv, reinterpret_cast<f4v*>(dst));
         } else if (ok[u]) {
           dst[0] = v[u].x;
           if (n[u] + 1 < N_b) dst[1] = v[u].y;
