@@ -87,6 +87,10 @@ struct RbFused {
   bool fused = false;         // this ResBlock runs as one resblock_bf16x3 launch
   bool m16 = false;           // ... on the 16x16x32 MFMA shape (resblock16_bf16x3)
   int kt = 0, halo = 0, W = 0, waves_n = 0;
+  // split into two launches (convs [0, split) then [split, n)): each part's window pays
+  // only its own receptive-field halo; the first writes x to scratch (0: one launch)
+  int split = 0;
+  int halo_p[2] = {0, 0}, W_p[2] = {0, 0};
   size_t w_off = 0, w_len = 0, b_off = 0, b_len = 0;  // in floats
 };
 
@@ -138,6 +142,8 @@ struct hfg_handle {
                      // warp-specialized conv_ws_bf16x3, measured ~3-15% slower than 3 on r01)
   bool use_fused_rb = true;
   bool rb64_narrow = true;   // 256-column whole-ResBlock window for C = 64, k = 3 (HFG_RB64_NARROW=0 disables)  // whole-ResBlock kernel for C in {32, 64} (HFG_FUSED_RB=0 disables)
+  bool rb_split = true;      // whole-ResBlock split in two launches where it cuts >= 10 % of the
+                             // halo recompute (k = 11 in V1; HFG_RB_SPLIT=0: off)
   int rb_waves_n32 = 4;      // window of the C = 32 ResBlock kernel: 128 * this columns
                              // (HFG_RB_WN32: 4 or 8)
   bool mfma16 = true;        // 16x16x32-shape ResBlock kernel for C = 32 (HFG_MFMA16=0: off)
@@ -437,6 +443,33 @@ int build_layers(hfg_handle* h) {
       rb.fused = true;
       // 16x16x32 shape: measured 3-4% faster for C = 32, 2-10% slower for C >= 64 (r01)
       rb.m16 = h->mfma16 && C == 32 && hfg::rb16_supported(C, rb.kt, waves_n);
+      // two launches where that cuts the MFMA work (windows / W, weighted by the convs of
+      // each part) by >= 10 %: the extra x write + read costs less than that at C <= 64
+      if (h->rb_split && C <= 64 && c.n_dil[j] >= 2) {
+        std::vector<int> hd;  // receptive-field radius of each dilation pair
+        for (int m = 0; m < c.n_dil[j]; ++m)
+          hd.push_back((rb.kt - 1) / 2 * c.dil[j][m] + (rb.kt - 1) / 2);
+        const double whole = (double)nwin / rb.W;
+        double best = whole;
+        for (int m = 1; m < c.n_dil[j]; ++m) {
+          int h0 = 0, h1 = 0;
+          for (int q = 0; q < m; ++q) h0 += hd[q];
+          for (int q = m; q < c.n_dil[j]; ++q) h1 += hd[q];
+          const int w0 = (nwin - 2 * h0) & ~3, w1 = (nwin - 2 * h1) & ~3;
+          if (w0 < nwin / 4 || w1 < nwin / 4) continue;
+          const double cost = ((double)m * nwin / w0 + (double)(c.n_dil[j] - m) * nwin / w1) /
+                              c.n_dil[j];
+          if (cost < best) {
+            best = cost;
+            rb.split = 2 * m;
+            rb.halo_p[0] = h0;
+            rb.halo_p[1] = h1;
+            rb.W_p[0] = w0;
+            rb.W_p[1] = w1;
+          }
+        }
+        if (best > 0.9 * whole) rb.split = 0;
+      }
       rb.w_off = off;
       rb.w_len = (size_t)rb.convs.size() * C * C * rb.kt;  // bf16 hi + lo = one float each
       off += (rb.w_len + 63) & ~(size_t)63;
@@ -1077,40 +1110,54 @@ int run_conv(hfg_handle* h, Launcher& ln, const Layer& L, const float* x, int64_
 }
 
 // One whole ResBlock (all dilations) + its MRF contribution in one launch.
+// A split ResBlock (rb.split) runs as two launches through `scratch` (B*C*L floats): convs
+// [0, split) write x after their dilation pairs (MRF-epilogue mode 0: a plain store), convs
+// [split, n) read it back and do the MRF epilogue.  fp32 round trip: bitwise the same x.
 int run_resblock(hfg_handle* h, Launcher& ln, const RbFused& rb, const float* x, int64_t B,
-                 int64_t Lt, float* mrf, int mrf_mode, float mrf_div, const int32_t* lens) {
+                 int64_t Lt, float* mrf, int mrf_mode, float mrf_div, const int32_t* lens,
+                 float* scratch) {
   const Layer& L0 = h->layers[rb.convs[0]];
   const int C = L0.C_out;
-  hfg::RbParams p{};
-  p.x = x;
-  p.bs = (int64_t)C * Lt;
-  p.L = (int)Lt;
-  p.len = lens;
-  p.w = reinterpret_cast<const __bf16*>(h->packed_dev + rb.w_off);
-  p.w_bytes = (int)(rb.w_len * sizeof(float));
-  p.bias = h->packed_dev + rb.b_off;
-  p.n_conv = (int)rb.convs.size();
-  double flop = 0.0;
-  for (int e = 0; e < p.n_conv; ++e) {
-    const Layer& L = h->layers[rb.convs[e]];
-    p.dil[e] = L.dil;
-    flop += 2.0 * L.C_out * L.C_in * L.k * (double)Lt * B;
+  const int n_all = (int)rb.convs.size();
+  const int n_part = rb.split && scratch ? 2 : 1;
+  for (int part = 0; part < n_part; ++part) {
+    const int c0 = n_part == 1 ? 0 : (part == 0 ? 0 : rb.split);
+    const int c1 = n_part == 1 ? n_all : (part == 0 ? rb.split : n_all);
+    const bool last = part == n_part - 1;
+    hfg::RbParams p{};
+    p.x = part == 0 ? x : scratch;
+    p.bs = (int64_t)C * Lt;
+    p.L = (int)Lt;
+    p.len = lens;
+    p.w = reinterpret_cast<const __bf16*>(h->packed_dev + rb.w_off);
+    p.w_bytes = (int)(rb.w_len * sizeof(float));
+    p.bias = h->packed_dev + rb.b_off + (size_t)c0 * C;
+    p.n_conv = c1 - c0;
+    p.conv0 = c0;
+    p.n_conv_stream = n_all;
+    double flop = 0.0;
+    for (int e = c0; e < c1; ++e) {
+      const Layer& L = h->layers[rb.convs[e]];
+      p.dil[e - c0] = L.dil;
+      flop += 2.0 * L.C_out * L.C_in * L.k * (double)Lt * B;
+    }
+    p.halo = n_part == 1 ? rb.halo : rb.halo_p[part];
+    p.W = n_part == 1 ? rb.W : rb.W_p[part];
+    p.mrf = last ? mrf : scratch;
+    p.mrf_mode = last ? mrf_mode : 0;
+    p.mrf_div = mrf_div;
+    p.dbg = h->dbg_flags;
+    const double bytes =
+        4.0 * B * Lt * C * ((last && (mrf_mode & 1)) ? 3 : 2) + 4.0 * (double)rb.w_len;
+    const char* name = nullptr;
+    ln.begin(flop, bytes);
+    hipError_t e =
+        rb.m16 ? hfg::launch_resblock16_bf16x3(C, rb.waves_n, rb.kt, h->np, p, (int)B, ln.stream, &name)
+               : hfg::launch_resblock_bf16x3(C, rb.waves_n, rb.kt, h->np, p, (int)B, ln.stream, &name);
+    ln.end(name);
+    if (e != hipSuccess)
+      return fail(HFG_EIO, "launch resblock %s: %s", L0.mod.c_str(), hipGetErrorString(e));
   }
-  p.halo = rb.halo;
-  p.W = rb.W;
-  p.mrf = mrf;
-  p.mrf_mode = mrf_mode;
-  p.mrf_div = mrf_div;
-  p.dbg = h->dbg_flags;
-  const double bytes = 4.0 * B * Lt * C * ((mrf_mode & 1) ? 3 : 2) + 4.0 * (double)rb.w_len;
-  const char* name = nullptr;
-  ln.begin(flop, bytes);
-  hipError_t e =
-      rb.m16 ? hfg::launch_resblock16_bf16x3(C, rb.waves_n, rb.kt, h->np, p, (int)B, ln.stream, &name)
-             : hfg::launch_resblock_bf16x3(C, rb.waves_n, rb.kt, h->np, p, (int)B, ln.stream, &name);
-  ln.end(name);
-  if (e != hipSuccess)
-    return fail(HFG_EIO, "launch resblock %s: %s", L0.mod.c_str(), hipGetErrorString(e));
   return HFG_OK;
 }
 
@@ -1233,7 +1280,8 @@ int run_one_rb(hfg_handle* h, Launcher& ln, const Stage& st, int j, int idx, con
                int64_t B, int64_t L, float* R, float* Tb, float* out, int mode,
                const int32_t* lens) {
   const hfg_config& c = h->cfg;
-  if (st.rbs[j].fused) return run_resblock(h, ln, st.rbs[j], X, B, L, out, mode, (float)c.n_res, lens);
+  if (st.rbs[j].fused)
+    return run_resblock(h, ln, st.rbs[j], X, B, L, out, mode, (float)c.n_res, lens, Tb);
   int rc;
   for (int m = 0; m < c.n_dil[j]; ++m, ++idx) {
     const float* src = (m == 0) ? X : R;
@@ -1505,6 +1553,7 @@ int create_impl(const hfg_config* cfg, bool mrf_only, int device, hfg_handle** o
   if (const char* ce = getenv("HFG_C16")) h->c16 = atoi(ce) != 0;
   if (const char* se = getenv("HFG_SPLIT")) h->split = atoi(se);
   if (const char* rn = getenv("HFG_RB64_NARROW")) h->rb64_narrow = atoi(rn) != 0;
+  if (const char* sp = getenv("HFG_RB_SPLIT")) h->rb_split = atoi(sp) != 0;
   if (const char* we = getenv("HFG_RB_WN32")) {
     const int v = atoi(we);
     if (v == 4 || v == 8) h->rb_waves_n32 = v;

@@ -191,7 +191,9 @@ struct RbParams {
   const __bf16* w;       // packed A stream [wave_m][conv][group][tap][plane][lane][8]
   int w_bytes;           // its size (buffer descriptor range)
   const float* bias;     // [conv][C]
-  int n_conv;            // 2 * n_dil, order conv1_0, conv2_0, conv1_1, ...
+  int n_conv;            // convs of this launch (even), order conv1_0, conv2_0, conv1_1, ...
+  int conv0;             // index of its first conv in the packed stream
+  int n_conv_stream;     // convs in the packed stream (the whole ResBlock)
   int dil[kRbMaxConv];   // dilation of each conv
   int halo, W;           // receptive-field radius, output columns per block
   float* mrf;            // MRF accumulator [B][C][L]

@@ -80,7 +80,10 @@ resblock16_bf16x3(const RbParams p) {
   const int cbase = wave_n * 16 * WN;      // first window column of this wave
   const int row0 = wave_m * 32;
   const int n_conv = p.n_conv;
-  const int QT = n_conv * STEPS;
+  // A stream: the whole ResBlock's convs (p.n_conv_stream per wave row-block); this launch
+  // runs convs p.conv0 .. p.conv0 + n_conv - 1 of it (a ResBlock split into two launches)
+  const int QT = p.n_conv_stream * STEPS;
+  const int Q0 = p.conv0 * STEPS;
   const int dbg = p.dbg;
   // channel row of accumulator element r of row tile i
   auto rrow = [&](int i, int r) { return row0 + 16 * i + 4 * quarter + r; };
@@ -111,8 +114,8 @@ resblock16_bf16x3(const RbParams p) {
           bf16x8, __builtin_amdgcn_raw_buffer_load_b128(wrs, a_lane + i * 2048 + 1024, so, 0));
     }
   };
-  load_a(0, 0);
-  load_a(1, 1);
+  load_a(0, Q0);
+  load_a(1, Q0 + 1);
 
   // ---- residual stream x: window -> registers (zero outside [0, len)) ----
   floatx4 xcur[WI][WN];
@@ -198,7 +201,7 @@ resblock16_bf16x3(const RbParams p) {
       bh[k % NB] = *reinterpret_cast<const bf16x8*>(src);
       bl[k % NB] = *reinterpret_cast<const bf16x8*>(src + PS);
     };
-    const int qb = cv * STEPS;
+    const int qb = Q0 + cv * STEPS;
     // one (step, column tile) unit: 6 MFMAs, the B fragment PF units ahead (the next
     // step's first ones clamped to the last step: a harmless re-read), and after the
     // step's last unit the A loads of step s + 2 into the step's ring slot SL
@@ -375,6 +378,7 @@ hipError_t launch_resblock16_bf16x3(int C, int waves_n, int kt, int np, const Rb
   if (!e || C % 32 != 0) return hipErrorInvalidValue;
   const int nwin = kRbColsPerWave * waves_n;
   if (p.n_conv < 2 || p.n_conv > kRbMaxConv || (p.n_conv & 1)) return hipErrorInvalidValue;
+  if (p.conv0 < 0 || p.conv0 + p.n_conv > p.n_conv_stream) return hipErrorInvalidValue;
   if (p.W <= 0 || p.halo < 0 || p.W + 2 * p.halo > nwin) return hipErrorInvalidValue;
   for (int i = 0; i < p.n_conv; ++i)
     if (p.dil[i] < 1 || (kt - 1) / 2 * p.dil[i] > rb_marg(C, waves_n)) return hipErrorInvalidValue;
