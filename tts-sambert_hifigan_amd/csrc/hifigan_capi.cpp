@@ -144,6 +144,7 @@ struct hfg_handle {
   bool rb64_narrow = true;   // 256-column whole-ResBlock window for C = 64, k = 3 (HFG_RB64_NARROW=0 disables)  // whole-ResBlock kernel for C in {32, 64} (HFG_FUSED_RB=0 disables)
   bool rb_split = true;      // whole-ResBlock split in two launches where it cuts >= 10 % of the
                              // halo recompute (k = 11 in V1; HFG_RB_SPLIT=0: off)
+  double rb_split_min = 0.9; // split when its MFMA work <= this x one launch's (HFG_RB_SPLIT_MIN)
   int rb_waves_n32 = 4;      // window of the C = 32 ResBlock kernel: 128 * this columns
                              // (HFG_RB_WN32: 4 or 8)
   bool mfma16 = true;        // 16x16x32-shape ResBlock kernel for C = 32 (HFG_MFMA16=0: off)
@@ -468,7 +469,7 @@ int build_layers(hfg_handle* h) {
             rb.W_p[1] = w1;
           }
         }
-        if (best > 0.9 * whole) rb.split = 0;
+        if (best > h->rb_split_min * whole) rb.split = 0;
       }
       rb.w_off = off;
       rb.w_len = (size_t)rb.convs.size() * C * C * rb.kt;  // bf16 hi + lo = one float each
@@ -1554,6 +1555,7 @@ int create_impl(const hfg_config* cfg, bool mrf_only, int device, hfg_handle** o
   if (const char* se = getenv("HFG_SPLIT")) h->split = atoi(se);
   if (const char* rn = getenv("HFG_RB64_NARROW")) h->rb64_narrow = atoi(rn) != 0;
   if (const char* sp = getenv("HFG_RB_SPLIT")) h->rb_split = atoi(sp) != 0;
+  if (const char* sm = getenv("HFG_RB_SPLIT_MIN")) h->rb_split_min = atof(sm);
   if (const char* we = getenv("HFG_RB_WN32")) {
     const int v = atoi(we);
     if (v == 4 || v == 8) h->rb_waves_n32 = v;
