@@ -46,16 +46,35 @@ def dev():
 
 @pytest.mark.parametrize("seed", range(N_CFG))
 def test_random_config(pkg, dev, seed):
+    """fp32 and bf16x3 against the oracle on the fp32 weights; bf16w against the oracle on
+    the bf16-rounded weights (the model bf16w computes); every third configuration loads
+    its weights in the apply_weight_norm layout (weight_g / weight_v)."""
     from oracle import config as C, hifigan_torch as H
     cfg, lens = _draw(seed)
-    sd = C.make_state_dict(cfg, seed=seed)
+    wn = seed % 3 == 2
+    sd = C.make_weight_norm_state_dict(cfg, seed=seed) if wn else C.make_state_dict(cfg, seed=seed)
+    # the plain weights the module folds g * v / ||v|| into (the reference's own fold)
+    probe = pkg.HiFiGANGenerator(**cfg.kwargs()).eval()
+    if wn:
+        probe.apply_weight_norm()
+    probe.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
+    if wn:
+        probe.remove_weight_norm()
+    plain = {k: v.detach().numpy().copy() for k, v in probe.state_dict().items()}
+    rounded = {k: (torch.from_numpy(v).to(torch.bfloat16).float().numpy() if k.endswith(".weight")
+                   else v) for k, v in plain.items()}
     T = max(lens)
     mel = torch.randn(len(lens), 80, T, generator=torch.Generator().manual_seed(seed))
-    refs = [H.generator_forward(H.to_torch_state(sd), cfg, mel[b:b + 1, :, :n])
-            for b, n in enumerate(lens)]
-    print(f"\nseed {seed}: {cfg} lens {lens}")
-    for precision in ("fp32", "bf16x3"):
+    refs_by = {}
+    for name, w in (("fp32", plain), ("bf16", rounded)):
+        refs_by[name] = [H.generator_forward(H.to_torch_state(w), cfg, mel[b:b + 1, :, :n])
+                         for b, n in enumerate(lens)]
+    print(f"\nseed {seed}: {cfg} lens {lens} weight_norm {wn}")
+    for precision in ("fp32", "bf16x3", "bf16w"):
+        refs = refs_by["bf16" if precision == "bf16w" else "fp32"]
         gen = pkg.HiFiGANGenerator(**cfg.kwargs(), precision=precision).eval()
+        if wn:
+            gen.apply_weight_norm()
         gen.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
         gen = gen.to(dev)
         try:
