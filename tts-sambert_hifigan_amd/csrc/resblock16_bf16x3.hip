@@ -286,55 +286,50 @@ resblock16_bf16x3(const RbParams p) {
   float* __restrict__ mb = p.mrf + (int64_t)b * p.bs;
   const bool add = p.mrf_mode & 1;
   const bool div = p.mrf_mode & 2;
+  // every column tile's MRF loads are issued before any store (see resblock_bf16x3.hip)
+  unsigned rowoff[WI][4];
 #pragma unroll
-  for (int k = 0; k < WN; k += 2) {
-    unsigned off[2][WI][4];
-    bool ok[2];
-    float v[2][WI][4];
+  for (int i = 0; i < WI; ++i)
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      const int c = cbase + 16 * (k + kk) + col;
-      ok[kk] = vk[k + kk] && c >= p.halo && c < p.halo + p.W;
-      const int ta = ws + c;
+    for (int r = 0; r < 4; ++r) rowoff[i][r] = (unsigned)(rrow(i, r) * p.L);
+  bool ok[WN];
+  unsigned ta[WN];
+#pragma unroll
+  for (int k = 0; k < WN; ++k) {
+    const int c = cbase + 16 * k + col;
+    ok[k] = vk[k] && c >= p.halo && c < p.halo + p.W;
+    ta[k] = ok[k] ? (unsigned)(ws + c) : 0u;
+  }
+  auto off = [&](int k, int i, int r) { return ok[k] ? rowoff[i][r] + ta[k] : 0u; };
+  if (add) {
+    float mv[WN][WI][4];
+#pragma unroll
+    for (int k = 0; k < WN; ++k)
 #pragma unroll
       for (int i = 0; i < WI; ++i)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          off[kk][i][r] = ok[kk] ? (unsigned)(rrow(i, r) * p.L + ta) : 0u;
-          v[kk][i][r] = xcur[i][k + kk][r];
-        }
-    }
-    if (add) {
-      float mv[2][WI][4];
+        for (int r = 0; r < 4; ++r) mv[k][i][r] = mb[off(k, i, r)];
 #pragma unroll
-      for (int kk = 0; kk < 2; ++kk)
+    for (int k = 0; k < WN; ++k)
 #pragma unroll
-        for (int i = 0; i < WI; ++i)
+      for (int i = 0; i < WI; ++i)
 #pragma unroll
-          for (int r = 0; r < 4; ++r) mv[kk][i][r] = mb[off[kk][i][r]];
+        for (int r = 0; r < 4; ++r) xcur[i][k][r] = mv[k][i][r] + xcur[i][k][r];
+  }
 #pragma unroll
-      for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-        for (int i = 0; i < WI; ++i)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) v[kk][i][r] = mv[kk][i][r] + v[kk][i][r];
-    }
+  for (int k = 0; k < WN; ++k) {
     if (div) {
 #pragma unroll
-      for (int kk = 0; kk < 2; ++kk)
+      for (int i = 0; i < WI; ++i)
 #pragma unroll
-        for (int i = 0; i < WI; ++i)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) v[kk][i][r] = v[kk][i][r] / p.mrf_div;
+        for (int r = 0; r < 4; ++r) xcur[i][k][r] = xcur[i][k][r] / p.mrf_div;
     }
+    if (ok[k]) {
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
-      if (ok[kk]) {
+      for (int i = 0; i < WI; ++i)
 #pragma unroll
-        for (int i = 0; i < WI; ++i)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) mb[off[kk][i][r]] = v[kk][i][r];
-      }
+        for (int r = 0; r < 4; ++r) mb[off(k, i, r)] = xcur[i][k][r];
+    }
   }
 }
 

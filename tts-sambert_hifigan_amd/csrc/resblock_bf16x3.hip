@@ -252,32 +252,42 @@ resblock_bf16x3(const RbParams p) {
   float* __restrict__ mb = p.mrf + (int64_t)b * p.bs;
   const bool add = p.mrf_mode & 1;
   const bool div = p.mrf_mode & 2;
+  // every column tile's MRF loads are issued before any store (the stores may alias later
+  // tiles' loads as far as the compiler knows, so a per-tile loop paid one HBM round trip
+  // per tile); the accumulators are dead here, so the 16 x WN loaded values fit
+  unsigned rowoff[16];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) rowoff[r] = (unsigned)((row0 + rrow(r)) * p.L);
+  bool ok[WN];
+  unsigned ta[WN];
 #pragma unroll
   for (int k = 0; k < WN; ++k) {
     const int c = cbase + 32 * k + col;
-    const bool ok = vk[k] && c >= p.halo && c < p.halo + p.W;
-    const int ta = ws + c;
-    unsigned off[16];
-    float v[16];
+    ok[k] = vk[k] && c >= p.halo && c < p.halo + p.W;
+    ta[k] = ok[k] ? (unsigned)(ws + c) : 0u;
+  }
+  // offsets formed at each access (one add) instead of 16 x WN live registers
+  auto off = [&](int k, int r) { return ok[k] ? rowoff[r] + ta[k] : 0u; };
+  if (add) {
+    float mv[WN][16];
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      off[r] = ok ? (unsigned)((row0 + rrow(r)) * p.L + ta) : 0u;
-      v[r] = xcur[k][r];
-    }
-    if (add) {
-      float mv[16];
+    for (int k = 0; k < WN; ++k)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) mv[r] = mb[off[r]];
+      for (int r = 0; r < 16; ++r) mv[k][r] = mb[off(k, r)];
 #pragma unroll
-      for (int r = 0; r < 16; ++r) v[r] = mv[r] + v[r];
-    }
+    for (int k = 0; k < WN; ++k)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) xcur[k][r] = mv[k][r] + xcur[k][r];
+  }
+#pragma unroll
+  for (int k = 0; k < WN; ++k) {
     if (div) {
 #pragma unroll
-      for (int r = 0; r < 16; ++r) v[r] = v[r] / p.mrf_div;
+      for (int r = 0; r < 16; ++r) xcur[k][r] = xcur[k][r] / p.mrf_div;
     }
-    if (ok) {
+    if (ok[k]) {
 #pragma unroll
-      for (int r = 0; r < 16; ++r) mb[off[r]] = v[r];
+      for (int r = 0; r < 16; ++r) mb[off(k, r)] = xcur[k][r];
     }
   }
 }
