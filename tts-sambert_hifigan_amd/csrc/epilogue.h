@@ -123,8 +123,34 @@ __device__ __forceinline__ void conv_epilogue_lds(const ConvParams& p, floatx16e
     __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's writes are in LDS
     __builtin_amdgcn_wave_barrier();
     constexpr int IT = 32 * C4 / 64;          // float4 per lane
+    // the residual / MRF loads of group it0 + 4 are issued before group it0's stores: the
+    // stores may alias later loads as far as the compiler knows, so loads placed after them
+    // cost one HBM round trip per group (same values, same additions in the same order)
+    float4 rvb[2][4], mvb[2][4];
+    auto geom = [&](int it, int& row, int& n, bool& ok) {
+      const int e = it * 64 + lane;
+      const int rr = e / C4, c4 = e - rr * C4;
+      row = row_base + i * 32 + rr;
+      n = n_base + 4 * c4;
+      ok = row < p.M && n < N_b;
+    };
+    auto load_group = [&](int it0, float4 (&rv)[4], float4 (&mv)[4]) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        int row, n;
+        bool ok;
+        geom(it0 + u, row, n, ok);
+        const int64_t o = (int64_t)row * p.N + n;
+        rv[u] = resb && ok ? *reinterpret_cast<const float4*>(resb + o) : float4{0.f, 0.f, 0.f, 0.f};
+        mv[u] = add_mrf && ok ? *reinterpret_cast<const float4*>(outb + o)
+                              : float4{0.f, 0.f, 0.f, 0.f};
+      }
+    };
+    load_group(0, rvb[0], mvb[0]);
 #pragma unroll
     for (int it0 = 0; it0 < IT; it0 += 4) {
+      const int cur = (it0 / 4) & 1;
+      if (it0 + 4 < IT) load_group(it0 + 4, rvb[cur ^ 1], mvb[cur ^ 1]);
       float4 v[4];
       int row[4], n[4];
       bool ok[4], full[4];
@@ -132,9 +158,7 @@ __device__ __forceinline__ void conv_epilogue_lds(const ConvParams& p, floatx16e
       for (int u = 0; u < 4; ++u) {
         const int e = (it0 + u) * 64 + lane;
         const int rr = e / C4, c4 = e - rr * C4;
-        row[u] = row_base + i * 32 + rr;
-        n[u] = n_base + 4 * c4;
-        ok[u] = row[u] < p.M && n[u] < N_b;
+        geom(it0 + u, row[u], n[u], ok[u]);
         full[u] = ok[u] && n[u] + 3 < N_b;
         v[u] = *reinterpret_cast<const float4*>(stage + rr * SROW + 4 * c4);
         const float bv = p.bias[row[u]];
@@ -144,17 +168,13 @@ __device__ __forceinline__ void conv_epilogue_lds(const ConvParams& p, floatx16e
         v[u].w += bv;
       }
       if (resb) {
-        float4 rv[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u)
-          rv[u] = ok[u] ? *reinterpret_cast<const float4*>(resb + (int64_t)row[u] * p.N + n[u])
-                        : float4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
-          v[u].x = rv[u].x + v[u].x;
-          v[u].y = rv[u].y + v[u].y;
-          v[u].z = rv[u].z + v[u].z;
-          v[u].w = rv[u].w + v[u].w;
+          const float4 rv = rvb[cur][u];
+          v[u].x = rv.x + v[u].x;
+          v[u].y = rv.y + v[u].y;
+          v[u].z = rv.z + v[u].z;
+          v[u].w = rv.w + v[u].w;
         }
       }
       if (act) {
@@ -167,17 +187,13 @@ __device__ __forceinline__ void conv_epilogue_lds(const ConvParams& p, floatx16e
         }
       }
       if (add_mrf) {
-        float4 mv[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u)
-          mv[u] = ok[u] ? *reinterpret_cast<const float4*>(outb + (int64_t)row[u] * p.N + n[u])
-                        : float4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
-          v[u].x = mv[u].x + v[u].x;
-          v[u].y = mv[u].y + v[u].y;
-          v[u].z = mv[u].z + v[u].z;
-          v[u].w = mv[u].w + v[u].w;
+          const float4 mv = mvb[cur][u];
+          v[u].x = mv.x + v[u].x;
+          v[u].y = mv.y + v[u].y;
+          v[u].z = mv.z + v[u].z;
+          v[u].w = mv.w + v[u].w;
         }
       }
       if (div_mrf) {
