@@ -165,6 +165,8 @@ struct hfg_handle {
   // batch split over two HIP streams (HFG_SPLIT=1 disables): the two halves' launches
   // overlap, so one half's ramp-down / epilogue tail runs beside the other's main loops
   int split = 2;
+  int64_t split_min_frames = 4096;  // batch frames from which a forward runs as two halves
+                                    // on two streams (HFG_SPLIT_MIN)
   hipStream_t aux = nullptr;
   hipEvent_t fork_ev = nullptr, join_ev = nullptr;
   // concurrent ResBlocks of small forwards (HFG_RB_CONC: -1 auto, 0 off, 1 whenever the
@@ -975,9 +977,8 @@ size_t ws_part_bytes(const hfg_handle* h, int64_t B, int64_t T, bool conc_ok = f
 }
 // small forwards stay on one stream: splitting them doubles an already latency-bound
 // launch count (measured: 32 x 62 frames 5.4 -> 5.6 ms split)
-constexpr int64_t kSplitMinFrames = 4096;
 bool split_batch(const hfg_handle* h, int64_t B, int64_t T) {
-  return h->split >= 2 && B >= 2 && B * T >= kSplitMinFrames;
+  return h->split >= 2 && B >= 2 && B * T >= h->split_min_frames;
 }
 // workspace of a forward: both halves' when the batch is split over two streams (whose
 // ResBlocks then run one after another), else one part with concurrent ResBlocks allowed
@@ -1553,6 +1554,7 @@ int create_impl(const hfg_config* cfg, bool mrf_only, int device, hfg_handle** o
   if (const char* ar = getenv("HFG_AREG")) h->areg = atoi(ar) != 0;
   if (const char* ce = getenv("HFG_C16")) h->c16 = atoi(ce) != 0;
   if (const char* se = getenv("HFG_SPLIT")) h->split = atoi(se);
+  if (const char* sm = getenv("HFG_SPLIT_MIN")) h->split_min_frames = atoll(sm);
   if (const char* rn = getenv("HFG_RB64_NARROW")) h->rb64_narrow = atoi(rn) != 0;
   if (const char* sp = getenv("HFG_RB_SPLIT")) h->rb_split = atoi(sp) != 0;
   if (const char* sm = getenv("HFG_RB_SPLIT_MIN")) h->rb_split_min = atof(sm);
