@@ -4,6 +4,10 @@
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
         --master-port P bench.py --gpus N --steps K --warmup W
 
+`--gpus N > 1` without a launcher environment starts the N ranks itself (torch.distributed.run
+as a child process, before this process touches the GPU); under an external launcher the
+WORLD_SIZE must equal N, or bench.py refuses to run (no mislabelled n_gpus).
+
 A step = one Generator forward of a [batch, 80, frames] synthetic mel per GPU
 (default batch 8 × 1024 frames = BASELINE config 2; 8 GPUs × 8 = config 3),
 mel and weights resident in HBM before the timed region.  Utterances are
@@ -264,12 +268,55 @@ def extra_configs(pkg, S, dev, precision, steps=5):
         return (time.perf_counter() - t0) / n
 
     def make(cfg):
+        # module defaults (verify_weights off: no per-forward host sync, hifigan.py)
         gen = pkg.HiFiGANGenerator(**cfg.kwargs(), precision=precision).eval()
         gen.load_state_dict({k: torch.from_numpy(v) for k, v in S.random_state_dict(cfg).items()})
-        # the weights do not change here: skip the module's per-forward content hash of the
-        # parameters (a D2H sync that catches edits through param.data; hifigan.py)
-        gen.verify_weights = False
         return gen.to(dev)
+
+    def module_vs_abi(gen, mel, n):
+        """gen(mel) as a reference user calls it vs the raw C ABI on preallocated buffers
+        (same handle, same streams): per-forward wall time of n back-to-back forwards, and
+        the host time of one call (the module's Python wrapper + the ABI's launches)."""
+        h = gen.hip_handle(dev)
+        B, _, T = mel.shape
+        out_len = h.out_len(T)
+        wav = torch.empty((B, 1, out_len), device=dev)
+        ws_b = h.workspace_bytes(B, T)
+        ws = torch.empty(ws_b, dtype=torch.uint8, device=dev)
+        st = torch.cuda.current_stream(dev).cuda_stream
+
+        def raw():
+            h.forward_ws(mel.data_ptr(), B, T, wav.data_ptr(), out_len, ws.data_ptr(), ws_b, st)
+
+        def mod():
+            gen(mel)
+
+        res = {}
+        for name, fn in (("abi", raw), ("module", mod)):
+            for _ in range(3):
+                fn()
+            res[name + "_ms"] = timed(fn, n) * 1e3
+            torch.cuda.synchronize(dev)
+            host = []
+            for _ in range(5):
+                t0 = time.perf_counter()
+                fn()
+                host.append(time.perf_counter() - t0)
+                torch.cuda.synchronize(dev)
+            res[name + "_host_us_per_call"] = sorted(host)[2] * 1e6
+        gen.verify_weights = True
+        for _ in range(2):
+            mod()
+        res["module_verify_weights_ms"] = timed(mod, n) * 1e3
+        gen.verify_weights = False
+        res["overhead_pct"] = 100.0 * (res["module_ms"] / res["abi_ms"] - 1.0)
+        res["overhead_us"] = 1e3 * (res["module_ms"] - res["abi_ms"])
+        res["note"] = ("gen(mel) through the drop-in module (defaults: no per-forward weight "
+                       "hash) vs hfg_forward_ws on preallocated buffers, n back-to-back forwards; "
+                       "host_us_per_call = wall time of one call (launches are asynchronous); "
+                       "module_verify_weights_ms = the opt-in content hash (a stream sync per "
+                       "forward)")
+        return res
 
     g = torch.Generator().manual_seed(1234)
     with torch.no_grad():
@@ -304,6 +351,31 @@ def extra_configs(pkg, S, dev, precision, steps=5):
         out["streaming_chunk_v1_64f"] = {"frames_in": 64 + 2 * ctx, "frames_emitted": 64,
                                          "ms": t_chunk * 1e3,
                                          "rtf": t_chunk / (64 * 256 / SAMPLE_RATE)}
+        out["module_forward_C1_1x80x256"] = module_vs_abi(gen, mel, 50)
+        # many concurrent streams batched into one forward per step (glue.StreamingVocoder
+        # with n_streams): steady state, every stream contributes one 64-frame chunk a step
+        for n_streams in (16, 64):
+            sv = glue.StreamingVocoder(gen, chunk_frames=64, n_streams=n_streams)
+            feed = torch.randn(n_streams, 80, 64, generator=g).to(dev)
+            for s_ in range(n_streams):
+                sv.feed(feed[s_, :, :ctx], s_)
+
+            def one_step():
+                for s_ in range(n_streams):
+                    sv.feed(feed[s_], s_)
+                return sv.step()
+
+            for _ in range(3):
+                one_step()
+            t_step = timed(one_step, 20)
+            out[f"streaming_{n_streams}_streams_v1_64f"] = {
+                "ms_per_step": t_step * 1e3, "streams": n_streams,
+                "chunk_latency_ms": t_step * 1e3,
+                "audio_s_per_wall_s": n_streams * 64 * 256 / SAMPLE_RATE / t_step,
+                "rtf_per_stream": t_step / (64 * 256 / SAMPLE_RATE),
+                "note": "glue.StreamingVocoder(n_streams): feed 64 frames to every stream, one "
+                        "step() = one batched forward of all chunks (64 + 2 x context frames "
+                        "each), bounded per-stream buffers; wall time incl. host work"}
         del gen
         gen = make(S.V2STAR)
         mel = torch.randn(16, 80, 2048, generator=g).to(dev)
@@ -314,6 +386,9 @@ def extra_configs(pkg, S, dev, precision, steps=5):
                                        "rtf": t / (16 * 2048 * 256 / SAMPLE_RATE)}
         del gen
         gen = make(S.V1)
+        mel8 = torch.randn(8, 80, 1024, generator=g).to(dev)
+        out["module_forward_C2_8x80x1024"] = module_vs_abi(gen, mel8, steps)
+        del mel8
         lens = [int(x) for x in torch.randint(60, 64, (32,), generator=g)]
         mel_pred = torch.randn(32, max(lens), 80, generator=g).to(dev)
         for _ in range(2):
@@ -344,20 +419,43 @@ def extra_configs(pkg, S, dev, precision, steps=5):
     return out
 
 
+def self_launch(args) -> int:
+    """`--gpus N > 1` without a launcher: start N rank processes of this same command
+    through torch.distributed.run (one process per GPU, rendezvous on 127.0.0.1) and
+    return its exit code.  Called before this process makes any GPU call (the ranks are
+    children; this process never initialises HIP)."""
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={args.gpus}", "--master-addr", "127.0.0.1",
+           "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, HFG_BENCH_SELF_LAUNCHED="1")
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC only on this host driver
+    print(f"[bench] launching {args.gpus} ranks: {' '.join(cmd[1:6])} ...", file=sys.stderr,
+          flush=True)
+    return subprocess.call(cmd, env=env)
+
+
 def main():
     args = parse()
+    if args.gpus > 1 and "RANK" not in os.environ:
+        sys.exit(self_launch(args))
     rank, world, local_rank = 0, 1, 0
-    if "RANK" in os.environ and int(os.environ.get("WORLD_SIZE", "1")) > 1:
-        rank, world, local_rank = (int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"]),
+    if "RANK" in os.environ:
+        rank, world, local_rank = (int(os.environ["RANK"]), int(os.environ.get("WORLD_SIZE", "1")),
                                    int(os.environ.get("LOCAL_RANK", "0")))
+    if world != args.gpus:
+        raise SystemExit(f"[bench] --gpus {args.gpus} but the launcher started WORLD_SIZE {world} "
+                         "ranks: refusing to report a mislabelled n_gpus")
     pmc, pmc_note = None, "not collected (--no-pmc or N > 1)"
     under_profiler = "rocprof" in os.environ.get("LD_PRELOAD", "")
     if world == 1 and not args.no_pmc and not args.pmc_child and not under_profiler:
         # before this process initialises the GPU: the passes are child processes
         pmc, pmc_note = pmc_traffic(["--preset", args.preset, "--batch", str(args.batch),
                                      "--frames", str(args.frames), "--precision", args.precision])
-    if world != args.gpus and rank == 0:
-        print(f"[bench] note: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
     assert torch.cuda.is_available(), "bench.py needs MI355X GPUs"
     dev_index = local_rank % torch.cuda.device_count()
     torch.cuda.set_device(dev_index)
@@ -367,6 +465,9 @@ def main():
             dist.init_process_group("nccl", device_id=dev)
         else:
             dist.init_process_group("gloo")
+        if dist.get_world_size() != args.gpus:
+            raise SystemExit(f"[bench] process group has {dist.get_world_size()} ranks, "
+                             f"--gpus {args.gpus}")
 
     pkg = ge.load_package()
     pkg.load_library()
@@ -436,9 +537,13 @@ def main():
             0.5 * (step_ms[len(step_ms) // 2 - 1] + step_ms[len(step_ms) // 2])
         if world > 1:
             dist.barrier()
-            t = torch.tensor([elapsed], dtype=torch.float64, device=coll_dev)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            elapsed = float(t.item())
+            t = torch.zeros(world, dtype=torch.float64, device=coll_dev)
+            t[rank] = elapsed
+            dist.all_reduce(t)  # every rank's time (the others contribute 0)
+            rank_ms[precision] = [1000.0 * float(v) / args.steps for v in t.tolist()]
+            elapsed = max(float(v) for v in t.tolist())
+        else:
+            rank_ms[precision] = [1000.0 * elapsed / args.steps]
         prof = {}
         if profile:
             if args.streams == 1:
@@ -491,6 +596,7 @@ def main():
                         "the copies are not overlapped with the next step's compute"}
 
     prof_ms = {}  # ms/step of the 1-stream roofline pass, per precision
+    rank_ms = {}  # per-rank ms/step of the value pass, per precision
     ev_median = {}  # per-step HIP-event median (ms) of the value pass, per precision
     e2e = {}
     elapsed, prof, out_len = measure(args.precision)
@@ -536,6 +642,11 @@ def main():
             "parallelism": f"dp{world} (utterance-sharded, RCCL weight broadcast at init)",
         },
         "value_per_gpu": value / world,
+        "per_rank_ms_per_step": rank_ms.get(args.precision),
+        "world_size_observed": dist.get_world_size() if world > 1 else 1,
+        "dist_backend": args.dist_backend if world > 1 else None,
+        "launch": ("self-launched torch.distributed.run" if os.environ.get("HFG_BENCH_SELF_LAUNCHED")
+                   else "external launcher" if world > 1 else "single process"),
         "value_note": "value = whole-job aggregate (all ranks' samples / max-over-ranks time, the "
                       "bench contract); value_per_gpu = value / n_gpus",
         "rtf": (elapsed / args.steps) / (args.batch * out_len / SAMPLE_RATE),

@@ -16,6 +16,18 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (HIP device); run with -m gpu")
 
 
+@pytest.fixture(scope="session", autouse=True)
+def _native_provenance(request):
+    """A GPU session must run the library built from this tree (hfg_version carries the
+    sha256 of csrc/ + include/ that build.py compiled in)."""
+    if not any(item.get_closest_marker("gpu") for item in request.session.items):
+        return
+    import __graft_entry__ as ge
+    p = ge.load_package()
+    print(f"\n[provenance] {p.load_library().hfg_version().decode()}")
+    p.check_provenance()
+
+
 @pytest.fixture(scope="session")
 def pkg():
     import __graft_entry__ as ge

@@ -206,22 +206,20 @@ def bf2f(u16):
     return (u16.astype(np.uint32) << 16).view(np.float32)
 
 
-@pytest.mark.parametrize("big_tile", ["0", "3", "4", "c16", "areg"])
+@pytest.mark.parametrize("big_tile", ["0", "3", "areg"])
 @pytest.mark.parametrize("preset", ["v1", "v2star"])
 def test_bf16x3_packing(pkg, preset, big_tile, monkeypatch):
     """bf16x3 layers: the packed hi/lo planes reconstruct every weight to ~2^-16
-    relative, in the fragment order of conv_bf16x3.hip (every tile for M >= 128), of
-    conv_ws_bf16x3.hip (4) and of conv16_bf16x3.hip (c16)."""
-    monkeypatch.setenv("HFG_C16", "1" if big_tile == "c16" else "0")
+    relative, in the fragment order of conv_bf16x3.hip (every tile for M >= 128)."""
     monkeypatch.setenv("HFG_AREG", "1" if big_tile == "areg" else "0")
-    monkeypatch.setenv("HFG_BF16X3_BIGTILE", "3" if big_tile in ("c16", "areg") else big_tile)
+    monkeypatch.setenv("HFG_BF16X3_BIGTILE", "3" if big_tile == "areg" else big_tile)
     cfg = C.PRESETS[preset]
     sd = C.make_state_dict(cfg, seed=31)
     h = host_handle(pkg, cfg, "bf16x3")
     for k, v in sd.items():
         h.set_weight(k, torch.from_numpy(v))
     h.commit()
-    # tile -> (WAVES_M, WM, TPC); ids 8 / 9 are conv_ws_bf16x3 / conv16_bf16x3 (kernels.h)
+    # tile -> (WAVES_M, WM, TPC)
     WAVES = {0: (2, 2, 4), 1: (1, 2, 2), 2: (1, 1, 4), 3: (2, 2, 2), 4: (2, 1, 4), 5: (2, 2, 2)}
     n_checked = 0
     for mod in ["conv_pre", "mrfs.0.resblocks.2.convs1.1", "mrfs.1.resblocks.0.convs2.1",
@@ -233,11 +231,6 @@ def test_bf16x3_packing(pkg, preset, big_tile, monkeypatch):
             assert cout < 32
             continue
         n_checked += 1
-        if info["tile"] in (8, 9):
-            rec = (unpack_ws if info["tile"] == 8 else unpack_c16)(info, packed)[:cout, :cin, :k]
-            assert np.abs(rec - W).max() / np.abs(W).max() < 2.0 ** -15, mod
-            assert np.array_equal(bias[:cout], sd[mod + ".bias"])
-            continue
         wm_, WM, TPC = WAVES[info["tile"]]
         MT = info["MT"]
         n_g, n_tg = -(-cin // 16), -(-k // TPC)
@@ -266,53 +259,8 @@ def test_bf16x3_packing(pkg, preset, big_tile, monkeypatch):
     assert n_checked >= 2
 
 
-def unpack_ws(info, packed):
-    """Invert conv_ws_bf16x3's stream order [m_tile][wave_m][g][tap][wm][plane][lane][8]
-    → Wt[row][ci][tap] (hi + lo, float64)."""
-    KT, n_g = info["KT"], info["n_chunks"]
-    u = packed.view(np.uint16).reshape(info["m_tiles"], 2, n_g, KT, 2, 2, 64, 8)
-    val = bf2f(u[:, :, :, :, :, 0]).astype(np.float64) + bf2f(u[:, :, :, :, :, 1])
-    Wt = np.zeros((info["m_tiles"] * 128, n_g * 16, KT))
-    lane = np.arange(64)
-    for mt in range(info["m_tiles"]):
-        for wv in range(2):
-            for wm in range(2):
-                rows = mt * 128 + wv * 64 + wm * 32 + (lane & 31)
-                for g in range(n_g):
-                    for e in range(8):
-                        Wt[rows, g * 16 + 8 * (lane >> 5) + e, :] = val[mt, wv, g, :, wm, lane, e]
-    return Wt[: info["M"]]
-
-
-def unpack_c16(info, packed):
-    """Invert conv16_bf16x3's per-k-step order [m_tile][step][plane][wave_m][row tile]
-    [lane][8] (entry f = 2*step + (lane >> 5) = (group f // KT, tap f % KT)) →
-    Wt[row][ci][tap] (hi + lo, float64)."""
-    KT, P = info["KT"], info["n_chunks"]
-    n_g = 2 * P // KT
-    assert n_g % 2 == 0 and n_g * KT == 2 * P
-    u = packed.view(np.uint16).reshape(info["m_tiles"], P, 2, 2, 4, 64, 8)
-    val = bf2f(u[:, :, 0]).astype(np.float64) + bf2f(u[:, :, 1])  # [mt][P][wv][i][lane][8]
-    Wt = np.zeros((info["m_tiles"] * 128, n_g * 16, KT))
-    lane = np.arange(64)
-    for mt in range(info["m_tiles"]):
-        for s in range(P):
-            f = 2 * s + (lane >> 5)
-            g, tap = f // KT, f % KT
-            for wv in range(2):
-                for i in range(4):
-                    rows = mt * 128 + wv * 64 + i * 16 + (lane & 15)
-                    for e in range(8):
-                        Wt[rows, g * 16 + 8 * ((lane >> 4) & 1) + e, tap] = val[mt, s, wv, i, :, e]
-    return Wt[: info["M"]]
-
-
 def unpack_bf16x3(info, packed, waves):
     """Invert conv_bf16x3's fragment order → Wt[row][ci][tap] (hi + lo, float64)."""
-    if info["tile"] == 8:
-        return unpack_ws(info, packed)
-    if info["tile"] == 9:
-        return unpack_c16(info, packed)
     wm_, WM, TPC = waves
     MT = info["MT"]
     n_chunks, KT = info["n_chunks"], info["KT"]
@@ -335,16 +283,14 @@ def unpack_bf16x3(info, packed, waves):
     return Wt[: info["M"], :, :KT]
 
 
-@pytest.mark.parametrize("c16", ["0", "1"])
-def test_bf16x3_polyphase_upsampler_packing(pkg, c16, monkeypatch):
-    monkeypatch.setenv("HFG_C16", c16)
+def test_bf16x3_polyphase_upsampler_packing(pkg):
     cfg = C.NONEXACT  # odd k-u on the first stages
     sd = C.make_state_dict(cfg, seed=41)
     h = host_handle(pkg, cfg, "bf16x3")
     for k, v in sd.items():
         h.set_weight(k, torch.from_numpy(v))
     h.commit()
-    waves = {0: (2, 2, 4), 1: (1, 2, 2), 2: (1, 1, 4), 3: (2, 2, 2), 4: (2, 1, 4), 8: None, 9: None}
+    waves = {0: (2, 2, 4), 1: (1, 2, 2), 2: (1, 1, 4), 3: (2, 2, 2), 4: (2, 1, 4)}
     rng = np.random.default_rng(1)
     c0 = cfg.upsample_initial_channel
     for i, (u, k) in enumerate(zip(cfg.upsample_rates, cfg.upsample_kernel_sizes)):
@@ -488,15 +434,14 @@ def _bf16_rne(a):
     return r.view(np.float32)
 
 
-@pytest.mark.parametrize("big_tile", ["3", "4", "c16"])
+@pytest.mark.parametrize("big_tile", ["0", "3"])
 @pytest.mark.parametrize("preset", ["v1", "v2star"])
 def test_bf16w_packing(pkg, preset, big_tile, monkeypatch):
     """HFG_DTYPE_BF16W: every conv weight is rounded to bf16 (nearest-even) when committed —
     the split layers' lo planes are all zero and their hi planes are exactly bf16(W); the
     fp32 layers (conv_post, C < 32 stages) hold the same bf16-valued weights; biases stay
-    fp32; the wide-tile / c16 variants (no NP 2 instances) are never chosen."""
-    monkeypatch.setenv("HFG_C16", "1" if big_tile == "c16" else "0")
-    monkeypatch.setenv("HFG_BF16X3_BIGTILE", "3" if big_tile == "c16" else big_tile)
+    fp32; the wide 8-wave tile (no NP 2 instance) is never chosen."""
+    monkeypatch.setenv("HFG_BF16X3_BIGTILE", big_tile)
     cfg = C.PRESETS[preset]
     sd = C.make_state_dict(cfg, seed=41)
     h = host_handle(pkg, cfg, "bf16w")
@@ -514,7 +459,7 @@ def test_bf16w_packing(pkg, preset, big_tile, monkeypatch):
         else:
             assert np.array_equal(bias[:W.shape[0]], sd[mod + ".bias"]), mod
         if info["CK"] == 16:
-            assert info["tile"] not in (8, 9), mod
+            assert info["tile"] != 0, mod
             n_split += 1
             u = packed.view(np.uint16)
             TPC = {0: 4, 1: 2, 2: 4, 3: 2, 4: 4, 5: 2}[info["tile"]]

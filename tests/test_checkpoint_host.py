@@ -90,3 +90,29 @@ def test_bad_layouts_rejected(pkg, ck):
     sd["resblocks.99.convs1.0.bias"] = torch.zeros(8)
     with pytest.raises(ValueError):
         ck.load_generator_checkpoint(gen, sd)
+
+
+def test_container_key_wins_over_stray_tensors(pkg, ck):
+    """{"state_dict": sd, "step": tensor, "ema_decay": tensor}: the container key is
+    unwrapped even though most top-level values are tensors."""
+    cfg = C.V2STAR
+    sd = _ref_weights(cfg, 12)
+    obj = {"state_dict": sd, "step": torch.tensor(1000), "ema_decay": torch.tensor(0.999)}
+    gen = pkg.HiFiGANGenerator(**cfg.kwargs())
+    res = ck.load_generator_checkpoint(gen, obj)
+    assert not res.missing_keys and not res.unexpected_keys
+    for k, v in sd.items():
+        assert torch.equal(gen.state_dict()[k], v), k
+
+
+def test_ddp_generator_inside_wrapper(pkg, ck):
+    """'generator.module.conv_pre.weight' (a DDP-wrapped generator inside the HiFiGAN
+    wrapper) loads: 'module.' is stripped again after 'generator.' (ADVICE r02)."""
+    cfg = C.V2STAR
+    sd = _ref_weights(cfg, 13)
+    obj = {"model": {"generator.module." + k: v for k, v in sd.items()}}
+    gen = pkg.HiFiGAN(**cfg.kwargs())
+    res = ck.load_generator_checkpoint(gen, obj)
+    assert not res.missing_keys and not res.unexpected_keys
+    for k, v in sd.items():
+        assert torch.equal(gen.generator.state_dict()[k], v), k

@@ -126,3 +126,75 @@ def test_ragged_sweep_equals_solo(pkg, dev, preset, precision):
                 ref = H.generator_forward(H.to_torch_state(sd), cfg, mel[b:b + 1, :, :n])
                 err = (solo.cpu() - ref).abs().max().item()
                 assert err < ATOL, (lens, b, err)
+
+
+def test_multi_stream_batched_equals_one_shot(pkg, gen_sd, dev):
+    """Several streams share each forward (one ragged batch per step, glue.StreamingVocoder
+    .step): every stream's audio is bitwise its one-shot run, whatever the push pattern."""
+    import importlib
+    glue = importlib.import_module("tts_sambert_hifigan_amd.glue")
+    gen, _ = gen_sd
+    lens = [230, 41, 1, 97, 64]
+    g = torch.Generator().manual_seed(12)
+    mels = [torch.randn(80, n, generator=g).to(dev) for n in lens]
+    refs = [run(gen, m[None])[0, 0] for m in mels]
+    S = len(mels)
+    sv = glue.StreamingVocoder(gen, chunk_frames=32, n_streams=S)
+    outs = {s: [] for s in range(S)}
+    pos = [0] * S
+    rng = np.random.default_rng(5)
+    batched = 0
+    while True:
+        for s in range(S):
+            if pos[s] < lens[s]:
+                n = int(rng.integers(1, 40))
+                sv.feed(mels[s][:, pos[s]:pos[s] + n], s)
+                pos[s] += n
+                if pos[s] >= lens[s]:
+                    sv.finish(s)
+        r = sv.step()
+        batched = max(batched, len(r))
+        for s, a in r.items():
+            outs[s].append(a)
+        if not r and all(p >= n for p, n in zip(pos, lens)):
+            break
+    torch.cuda.synchronize()
+    assert batched > 1
+    for s in range(S):
+        assert torch.equal(torch.cat(outs[s]), refs[s]), s
+
+
+def test_ten_minute_stream_constant_memory(pkg, dev):
+    """A 10-minute stream (51,680 frames at 22.05 kHz / hop 256) in 64-frame pushes: the
+    buffer is allocated once, device memory does not grow after the first chunks, and the
+    streamed audio is bitwise the one-shot forward of the whole utterance."""
+    import importlib
+    glue = importlib.import_module("tts_sambert_hifigan_amd.glue")
+    from oracle import config as C
+    sd = C.make_state_dict(C.V1, seed=4)
+    gen = pkg.HiFiGANGenerator(**C.V1.kwargs(), precision="bf16x3").eval()
+    gen.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
+    gen = gen.to(dev)
+    T = 22050 * 600 // 256
+    mel = torch.randn(80, T, generator=torch.Generator().manual_seed(2)).to(dev)
+    sv = glue.StreamingVocoder(gen, chunk_frames=64)
+    out = torch.empty(T * 256, device=dev)
+    pos, w, caps, mem = 0, 0, set(), []
+    while pos < T:
+        a = sv.push(mel[:, pos:pos + 64])
+        out[w:w + a.numel()] = a
+        w += a.numel()
+        pos += 64
+        caps.add(sv.capacity())
+        if pos // 64 in (50, 400, 800):
+            torch.cuda.synchronize()
+            mem.append(torch.cuda.memory_allocated(dev))
+    a = sv.flush()
+    out[w:w + a.numel()] = a
+    w += a.numel()
+    torch.cuda.synchronize()
+    assert w == T * 256
+    assert len(caps) == 1 and sv.buffered_frames() <= 64 + 2 * sv.ctx
+    assert mem[-1] <= mem[0], mem
+    ref = run(gen, mel[None])[0, 0]
+    assert torch.equal(out, ref)

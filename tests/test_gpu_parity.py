@@ -96,19 +96,17 @@ def test_golden_fixture_bf16x3(pkg, golden_index, name):
 
 
 @pytest.mark.parametrize("big_tile,fused,wn32,m16",
-                         [("4", "1", "4", "1"), ("4", "0", "8", "0"), ("3", "1", "4", "1"),
-                          ("3", "1", "8", "0"), ("0", "1", "8", "1"), ("c16", "1", "4", "1"),
-                          ("c16", "0", "4", "1")])
+                         [("3", "1", "4", "1"), ("3", "0", "8", "0"), ("3", "1", "8", "0"),
+                          ("0", "1", "8", "1"), ("0", "0", "4", "1")])
 @pytest.mark.parametrize("preset,B,T", [("v1", 2, 300), ("v2star", 2, 200)])
 def test_bf16x3_vs_oracle_longer(pkg, preset, B, T, big_tile, fused, wn32, m16, monkeypatch):
     """Random weights/mel vs the oracle, with each tile choice for the M >= 128 layers
-    (HFG_BF16X3_BIGTILE: 0 = 128x256 8-wave, 3 = 128x256 4-wave, 4 = warp-specialized
-    128x256, default) and with the
+    (HFG_BF16X3_BIGTILE: 0 = 128x256 8-wave, 3 = 128x256 4-wave with layer convs on tile 5
+    — the default) and with the
     whole-ResBlock kernel for C in {32, 64} on (HFG_FUSED_RB=1, default; C = 32 window
     512 or 1024 columns) or off (layer per launch)."""
     from oracle import config as C, prng
-    monkeypatch.setenv("HFG_C16", "1" if big_tile == "c16" else "0")
-    monkeypatch.setenv("HFG_BF16X3_BIGTILE", "3" if big_tile == "c16" else big_tile)
+    monkeypatch.setenv("HFG_BF16X3_BIGTILE", big_tile)
     monkeypatch.setenv("HFG_FUSED_RB", fused)
     monkeypatch.setenv("HFG_RB_WN32", wn32)
     monkeypatch.setenv("HFG_MFMA16", m16)

@@ -303,14 +303,20 @@ def test_over_max_length_rejected(pkg, v1, dev):
 # ---- weight tracking and 2-stream capture -------------------------------------------
 def test_weight_edit_through_data_is_picked_up(pkg, dev):
     """An in-place edit through ``param.data`` leaves autograd's version counter alone;
-    the module's content hash (hfg_checksum32) still notices it, so the next forward
-    runs on the new weights.  Same for a ResBlock on its own."""
+    with ``verify_weights`` on (opt-in since round 3: it costs a host sync per forward) the
+    module's content hash (hfg_checksum32) still notices it, so the next forward runs on
+    the new weights.  Same for a ResBlock on its own.  By default the
+    version / data_ptr fingerprint is the only check and ``refresh_weights()`` is the
+    route for ``.data`` edits."""
     from oracle import config as C, hifigan_torch as H, prng
     cfg = C.V2STAR
     sd = C.make_state_dict(cfg, seed=8)
     gen = pkg.HiFiGANGenerator(**cfg.kwargs()).eval()
     gen.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
     gen = gen.to(dev)
+    assert gen.verify_weights is False  # default: no per-forward hash / host sync
+    gen.verify_weights = True
+    gen.mrfs[0].resblocks[1].verify_weights = True
     mel = torch.from_numpy(prng.mel_input(8, (1, 80, 20))).to(dev)
     w0 = run(gen, mel).clone()
     v0 = gen.ups[1].weight._version

@@ -208,6 +208,25 @@ def load_library(path: str = LIB_PATH):
     return lib
 
 
+def library_source_hash(lib=None) -> str:
+    """The source-tree hash compiled into the loaded library (hfg_version "src:...")."""
+    v = (lib or load_library()).hfg_version().decode()
+    return v.rsplit("src:", 1)[-1] if "src:" in v else ""
+
+
+def check_provenance(lib=None) -> str:
+    """Raise unless the loaded libhifigan_hip.so was built from THIS tree's csrc/ and
+    include/ (the sha256 build.py computes over them == the one compiled into
+    hfg_version).  Returns the hash.  Used by smoke() and the GPU test session."""
+    from .build import source_hash
+    want, got = source_hash(), library_source_hash(lib)
+    if want != got:
+        raise HipExtensionMissing(
+            f"{LIB_PATH} was built from source tree {got or '?'}, this tree is {want}: "
+            "rebuild it (python tts-sambert_hifigan_amd/build.py)")
+    return got
+
+
 def check(rc: int):
     if rc != 0:
         msg = load_library().hfg_last_error().decode(errors="replace")

@@ -4,6 +4,7 @@
 """
 from __future__ import annotations
 
+import hashlib
 import os
 import subprocess
 import sys
@@ -13,11 +14,9 @@ PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(PKG_DIR, "csrc")
 LIB_NAME = "libhifigan_hip.so"
 LIB_PATH = os.path.join(PKG_DIR, LIB_NAME)
-SOURCES = ["conv_kernels.hip", "conv_bf16x3.hip", "conv16_bf16x3.hip", "resblock_bf16x3.hip",
-           "resblock16_bf16x3.hip", "mrf_thin.hip", "mrf_thin_mfma.hip",
-           "conv_ws_bf16x3.hip", "probe.hip", "hifigan_capi.cpp", "mel_kernels.hip", "mel_capi.cpp"]
-HEADERS = ["kernels.h", "mel_kernels.h", "epilogue.h", "bf16x3_common.h", os.path.join("..", "..", "include", "hifigan_hip.h"),
-           os.path.join("..", "..", "include", "hifigan_hip_inspect.h")]
+SOURCES = ["conv_kernels.hip", "conv_bf16x3.hip", "resblock_bf16x3.hip", "resblock16_bf16x3.hip",
+           "mrf_thin.hip", "mrf_thin_mfma.hip", "probe.hip", "hifigan_capi.cpp", "mel_kernels.hip",
+           "mel_capi.cpp"]
 
 OBJ_DIR = os.path.join(PKG_DIR, "build")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
@@ -30,43 +29,89 @@ FLAGS = [
 ]
 
 
-def _stale() -> bool:
-    if not os.path.exists(LIB_PATH):
+def _tree_files():
+    """Every file the library is built from: csrc/* (sources and headers) and include/*.h."""
+    inc = os.path.join(PKG_DIR, "..", "include")
+    files = [os.path.join(CSRC, f) for f in os.listdir(CSRC)
+             if f.endswith((".hip", ".cpp", ".h"))]
+    files += [os.path.join(inc, f) for f in os.listdir(inc) if f.endswith(".h")]
+    return sorted(files, key=os.path.basename)
+
+
+def source_hash() -> str:
+    """16 hex digits of sha256 over the build inputs (file names + contents of csrc/ and
+    include/, the compiler flags).  Embedded in the library (``hfg_version``) so a loaded
+    binary can be matched to the tree it claims to come from."""
+    h = hashlib.sha256()
+    for f in _tree_files():
+        h.update(os.path.basename(f).encode() + b"\0")
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+        h.update(b"\0")
+    h.update(" ".join(FLAGS).encode())
+    return h.hexdigest()[:16]
+
+
+def _obj_key(src: str, tree: str) -> str:
+    """What an object depends on: its source, every header, the flags (and, for the C ABI
+    unit that embeds it, the tree hash)."""
+    h = hashlib.sha256()
+    for f in [os.path.join(CSRC, src)] + [f for f in _tree_files() if f.endswith(".h")]:
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    h.update(" ".join(FLAGS).encode())
+    if src == "hifigan_capi.cpp":
+        h.update(tree.encode())
+    return h.hexdigest()
+
+
+def _stale(tree: str) -> bool:
+    stamp = os.path.join(OBJ_DIR, "lib.stamp")
+    if not os.path.exists(LIB_PATH) or not os.path.exists(stamp):
         return True
-    t = os.path.getmtime(LIB_PATH)
-    deps = [os.path.join(CSRC, s) for s in SOURCES] + [os.path.join(CSRC, h) for h in HEADERS]
-    return any(os.path.exists(d) and os.path.getmtime(d) > t for d in deps)
+    with open(stamp) as f:
+        return f.read().strip() != tree
 
 
 def _obj(src: str) -> str:
     return os.path.join(OBJ_DIR, os.path.splitext(src)[0] + ".o")
 
 
-def _compile(src: str, verbose: bool):
-    cmd = [HIPCC, *FLAGS, "-c", os.path.join(CSRC, src), "-o", _obj(src) + ".tmp"]
+def _compile(src: str, verbose: bool, tree: str):
+    extra = [f'-DHFG_SRC_HASH="{tree}"'] if src == "hifigan_capi.cpp" else []
+    cmd = [HIPCC, *FLAGS, *extra, "-c", os.path.join(CSRC, src), "-o", _obj(src) + ".tmp"]
     if verbose:
         print("[build]", " ".join(cmd), flush=True)
     res = subprocess.run(cmd, capture_output=True, text=True)
     if res.returncode != 0:
         return src, res.stdout + res.stderr
     os.replace(_obj(src) + ".tmp", _obj(src))
+    with open(_obj(src) + ".key", "w") as f:
+        f.write(_obj_key(src, tree))
     return src, None
 
 
 def build(force: bool = False, verbose: bool = True) -> str:
     """Compile the HIP kernels + C ABI into ``libhifigan_hip.so`` next to this file: one
-    object per source (in parallel, only the stale ones), then one link."""
-    if not force and not _stale():
+    object per source (in parallel, only those whose inputs' CONTENT changed — not
+    mtimes, which a copied tree does not preserve), then one link.  The tree hash is
+    compiled into ``hfg_version`` and written to ``build/lib.stamp``."""
+    tree = source_hash()
+    if not force and not _stale(tree):
         return LIB_PATH
     os.makedirs(OBJ_DIR, exist_ok=True)
-    hdr_t = max(os.path.getmtime(os.path.join(CSRC, h)) for h in HEADERS
-                if os.path.exists(os.path.join(CSRC, h)))
-    todo = [src for src in SOURCES
-            if force or not os.path.exists(_obj(src))
-            or os.path.getmtime(_obj(src)) < max(hdr_t, os.path.getmtime(os.path.join(CSRC, src)))]
+
+    def obj_stale(src):
+        if force or not os.path.exists(_obj(src)) or not os.path.exists(_obj(src) + ".key"):
+            return True
+        with open(_obj(src) + ".key") as f:
+            return f.read().strip() != _obj_key(src, tree)
+
+    todo = [src for src in SOURCES if obj_stale(src)]
     jobs = max(1, min(len(todo), int(os.environ.get("MAX_JOBS", "8"))))
     with ThreadPoolExecutor(jobs) as ex:
-        errs = [(src, err) for src, err in ex.map(lambda s_: _compile(s_, verbose), todo) if err]
+        errs = [(src, err) for src, err in ex.map(lambda s_: _compile(s_, verbose, tree), todo)
+                if err]
     if errs:
         for src, err in errs:
             sys.stderr.write(f"--- {src}\n{err}")
@@ -81,6 +126,8 @@ def build(force: bool = False, verbose: bool = True) -> str:
         sys.stderr.write(res.stdout + res.stderr)
         raise RuntimeError(f"hipcc link failed with exit code {res.returncode}")
     os.replace(tmp, LIB_PATH)
+    with open(os.path.join(OBJ_DIR, "lib.stamp"), "w") as f:
+        f.write(tree)
     return LIB_PATH
 
 

@@ -34,13 +34,16 @@ _CONTAINER_KEYS = ("generator", "state_dict", "model", "model_state_dict")
 
 
 def _unwrap(obj) -> Dict[str, torch.Tensor]:
+    """The tensor mapping inside a checkpoint.  Known container keys win over the
+    "mostly tensors" heuristic, so ``{"state_dict": sd, "step": tensor, "ema": tensor}``
+    unwraps to ``sd`` rather than returning the stray tensors."""
     if isinstance(obj, Mapping):
-        tensors = {k: v for k, v in obj.items() if isinstance(v, torch.Tensor)}
-        if tensors and len(tensors) >= len(obj) // 2:
-            return dict(tensors)
         for key in _CONTAINER_KEYS:
             if key in obj and isinstance(obj[key], Mapping):
                 return _unwrap(obj[key])
+        tensors = {k: v for k, v in obj.items() if isinstance(v, torch.Tensor)}
+        if tensors and len(tensors) >= len(obj) // 2:
+            return dict(tensors)
     raise ValueError("no state dict found in the checkpoint (expected a tensor mapping or one of "
                      f"{_CONTAINER_KEYS})")
 
@@ -67,9 +70,12 @@ def convert_state_dict(obj, num_kernels: int, num_upsamples: int,
     weight-normalises (ups, ResBlock convs) for a Generator on which
     ``apply_weight_norm()`` was called; otherwise every pair is folded."""
     sd = _unwrap(obj)
-    sd = {re.sub(r"^(module\.)+", "", k): v for k, v in sd.items()}
+    strip = re.compile(r"^(module\.)+")
+    sd = {strip.sub("", k): v for k, v in sd.items()}
     if any(k.startswith("generator.") for k in sd):
-        sd = {k[len("generator."):]: v for k, v in sd.items() if k.startswith("generator.")}
+        # a DDP-wrapped generator inside the wrapper: generator.module.conv_pre.weight
+        sd = {strip.sub("", k[len("generator."):]): v for k, v in sd.items()
+              if k.startswith("generator.")}
     sd = {k: v for k, v in sd.items() if not k.startswith(("msd.", "mpd."))}
     flat = re.compile(r"^resblocks\.(\d+)\.(.*)$")
     out = {}

@@ -20,6 +20,8 @@
 // is multiplied), one barrier per chunk.  Epilogue identical to conv1d_mfma_f32.
 #include <hip/hip_runtime.h>
 
+#include <mutex>
+
 #include <algorithm>
 
 #include <cstdio>
@@ -725,12 +727,11 @@ struct Entry3 {
   bool ups;
   int np;
   ConvFn3 fn;
-  bool attr;
   char name[96];
 };
 
 #define HFG3_ENTRY(KT, TILE, UPS, NP) \
-  { KT, TILE, UPS, NP, Inst3<KT, TILE, UPS, NP>::fn(), false, {0} }
+  { KT, TILE, UPS, NP, Inst3<KT, TILE, UPS, NP>::fn(), {0} }
 #define HFG3_TILES(KT, UPS)                                                                  \
   HFG3_ENTRY(KT, 0, UPS, 3), HFG3_ENTRY(KT, 1, UPS, 3), HFG3_ENTRY(KT, 2, UPS, 3),           \
       HFG3_ENTRY(KT, 3, UPS, 3), HFG3_ENTRY(KT, 4, UPS, 3), HFG3_ENTRY(KT, 1, UPS, 2),       \
@@ -774,20 +775,19 @@ hipError_t launch_conv_bf16x3(int tile, int kt, bool ups, int np, const ConvPara
   if (p.dil > kMaxDil || (e->kt == 0 && kt > 16) || (kt - 1) * p.dil > kBf16x3MaxHalo)
     return hipErrorInvalidValue;
   const Bf16x3Cfg& t = kBf16x3Tiles[tile];
-  if (!e->name[0])
-    snprintf(e->name, sizeof(e->name), "conv1d_bf16x3<%d, %d, %d, %d, %d, %d, %d, %s, %d%s>",
-             e->kt, t.TPC, t.WAVES_M, t.WAVES_N, t.WM, t.WN, t.WD, e->ups ? "true" : "false",
-             e->np, t.AREG ? ", true" : "");
+  {
+    std::lock_guard<std::mutex> lk(setup_mutex());
+    if (!e->name[0])
+      snprintf(e->name, sizeof(e->name), "conv1d_bf16x3<%d, %d, %d, %d, %d, %d, %d, %s, %d%s>",
+               e->kt, t.TPC, t.WAVES_M, t.WAVES_N, t.WM, t.WN, t.WD, e->ups ? "true" : "false",
+               e->np, t.AREG ? ", true" : "");
+  }
   size_t lds = bf16x3_lds_bytes(tile, kt, p.dil);
   if (p.epi_lds && !ups)
     lds = std::max(lds, (size_t)t.threads() / 64 * 32 * (32 * t.WN + 8) * sizeof(float));
   if (lds > 160 * 1024) return hipErrorInvalidValue;
-  if (!e->attr) {
-    hipError_t err = hipFuncSetAttribute(reinterpret_cast<const void*>(e->fn),
-                                         hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    if (err != hipSuccess) return err;
-    e->attr = true;
-  }
+  if (hipError_t err = ensure_max_lds(reinterpret_cast<const void*>(e->fn)))
+    return err;
   if (name) *name = e->name;
   dim3 grid(n_tiles, m_tiles, batch);
   e->fn<<<grid, dim3(t.threads()), lds, stream>>>(p);

@@ -26,6 +26,8 @@
 // an HBM-bound reduction over C*7 inputs per sample, LDS-staged.
 #include <hip/hip_runtime.h>
 
+#include <mutex>
+
 #include <algorithm>
 
 #include <cstdio>
@@ -320,12 +322,11 @@ struct Entry {
   int tile;
   bool ups;
   ConvFn fn;
-  bool lds_attr_set;
   char name[96];  // template-instance name as rocprofv3 prints it
 };
 
 #define HFG_ENTRY(KT, TILE, UPS) \
-  { KT, TILE, UPS, Inst<KT, TILE, UPS>::fn(), false, {0} }
+  { KT, TILE, UPS, Inst<KT, TILE, UPS>::fn(), {0} }
 
 #define HFG_ENTRIES_KT(KT, UPS) \
   HFG_ENTRY(KT, 0, UPS), HFG_ENTRY(KT, 1, UPS), HFG_ENTRY(KT, 2, UPS)
@@ -351,9 +352,12 @@ hipError_t launch_conv(TileId tile, int kt, bool ups, const ConvParams& p, int n
   if (!e) return hipErrorInvalidValue;
   const TileCfg& t = kTiles[tile];
   const int ck = ck_for(e->kt, tile);
-  if (!e->name[0])
-    snprintf(e->name, sizeof(e->name), "conv1d_mfma_f32<%d, %d, %d, %d, %d, %d, %s>", e->kt, t.WM,
-             t.WN, t.WAVES_M, t.WAVES_N, ck, e->ups ? "true" : "false");
+  {
+    std::lock_guard<std::mutex> lk(setup_mutex());
+    if (!e->name[0])
+      snprintf(e->name, sizeof(e->name), "conv1d_mfma_f32<%d, %d, %d, %d, %d, %d, %s>", e->kt, t.WM,
+               t.WN, t.WAVES_M, t.WAVES_N, ck, e->ups ? "true" : "false");
+  }
   if ((kt - 1) * p.dil > halo_max(e->kt)) return hipErrorInvalidValue;
   const int xw = t.NTILE() + (kt - 1) * p.dil;
   const size_t stage = (size_t)t.MT() * ck * kt + (((size_t)ck * xw + 3) & ~(size_t)3);
@@ -363,12 +367,8 @@ hipError_t launch_conv(TileId tile, int kt, bool ups, const ConvParams& p, int n
   const size_t epi = sizeof(float) * (size_t)t.threads() / 64 * 32 * (32 * t.WN + 8);
   if (ups || epi > lds) pe.epi_lds = 0;
   if (lds > 160 * 1024) return hipErrorInvalidValue;
-  if (lds > 64 * 1024 && !e->lds_attr_set) {
-    hipError_t err = hipFuncSetAttribute(reinterpret_cast<const void*>(e->fn),
-                                         hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    if (err != hipSuccess) return err;
-    e->lds_attr_set = true;
-  }
+  if (hipError_t err = ensure_max_lds(reinterpret_cast<const void*>(e->fn)))
+    return err;
   if (name) *name = e->name;
   dim3 grid(n_tiles, m_tiles, batch);
   e->fn<<<grid, dim3(t.threads()), lds, stream>>>(pe);
@@ -380,13 +380,8 @@ hipError_t launch_conv_post(const float* x, int64_t x_bs, int C, int L, const fl
                             hipStream_t stream, const char** name) {
   const size_t lds = conv_post_lds_bytes(C);
   if (lds > 160 * 1024) return hipErrorInvalidValue;
-  static bool attr = false;
-  if (lds > 64 * 1024 && !attr) {
-    hipError_t err = hipFuncSetAttribute(reinterpret_cast<const void*>(conv_post_tanh),
-                                         hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    if (err != hipSuccess) return err;
-    attr = true;
-  }
+  if (hipError_t err = ensure_max_lds(reinterpret_cast<const void*>(conv_post_tanh)))
+    return err;
   if (name) *name = "conv_post_tanh";
   dim3 grid((L + 255) / 256, batch);
   conv_post_tanh<<<grid, dim3(256), lds, stream>>>(x, x_bs, C, L, w, bias, wav, lens);

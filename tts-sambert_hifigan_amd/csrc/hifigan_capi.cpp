@@ -13,6 +13,7 @@
 #include <cstring>
 #include <map>
 #include <mutex>
+#include <set>
 #include <string>
 #include <tuple>
 #include <vector>
@@ -20,6 +21,24 @@
 #include "../../include/hifigan_hip.h"
 #include "../../include/hifigan_hip_inspect.h"
 #include "kernels.h"
+
+namespace hfg {
+std::mutex& setup_mutex() {
+  static std::mutex mu;
+  return mu;
+}
+hipError_t ensure_max_lds(const void* fn) {
+  static std::set<std::pair<const void*, int>> done;
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return e;
+  std::lock_guard<std::mutex> lk(setup_mutex());
+  if (done.count({fn, dev})) return hipSuccess;
+  e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  if (e == hipSuccess) done.insert({fn, dev});
+  return e;
+}
+}  // namespace hfg
 
 using hfg::ConvParams;
 using hfg::kTiles;
@@ -138,8 +157,7 @@ struct hfg_handle {
   void* ws = nullptr;
   size_t ws_bytes = 0;
   bool profiling = false;
-  int big_tile = 3;  // bf16x3 tile for M >= 128 (HFG_BF16X3_BIGTILE env: 0, 3 or 4 =
-                     // warp-specialized conv_ws_bf16x3, measured ~3-15% slower than 3 on r01)
+  int big_tile = 3;  // bf16x3 tile for M >= 128 (HFG_BF16X3_BIGTILE env: 0 or 3)
   bool use_fused_rb = true;
   bool rb64_narrow = true;   // 256-column whole-ResBlock window for C = 64, k = 3 (HFG_RB64_NARROW=0 disables)  // whole-ResBlock kernel for C in {32, 64} (HFG_FUSED_RB=0 disables)
   bool rb_split = true;      // whole-ResBlock split in two launches where it cuts >= 10 % of the
@@ -159,8 +177,6 @@ struct hfg_handle {
                              // (HFG_THIN_MFMA)
   bool thin = true;          // whole-MRF VALU kernel for C <= 16 stages (HFG_THIN=0: layer
                              // kernels instead)
-  bool c16 = false;          // 16x16x32-shape wide layer kernel conv16_bf16x3 (HFG_C16=1;
-                             // parity-green, measured 26-45% slower than tile 3 on r01)
   int dbg_flags = 0;  // HFG_DEBUG_FLAGS env (kernel ablations; wrong results when set)
   // batch split over two HIP streams (HFG_SPLIT=1 disables): the two halves' launches
   // overlap, so one half's ramp-down / epilogue tail runs beside the other's main loops
@@ -326,42 +342,9 @@ int build_layers(hfg_handle* h) {
       continue;
     }
     if (split_dtype(h->cfg.dtype) && (L.kind == L_CONV || L.kind == L_UPS) &&
-        h->big_tile == hfg::kWsTile && hfg::ws_supported(L.KT, L.kind == L_UPS, L.M, L.dil)) {
-      // warp-specialized path: A stream [m_tile][wave_m][group][tap][plane][lane][8]
-      L.prec = 1;
-      L.tile = hfg::kWsTile;
-      L.CK = hfg::kBf16x3Ck;
-      L.m_tiles = L.M / hfg::kWsMT;
-      L.n_chunks = (L.C_in + 15) / 16;
-      L.w_off = off;
-      L.w_len = (size_t)L.m_tiles * 4 * L.n_chunks * L.KT * 1024 / 2;  // bf16 pairs as floats
-      off += (L.w_len + 63) & ~(size_t)63;
-      L.b_off = off;
-      L.b_len = (size_t)L.m_tiles * hfg::kWsMT;
-      off += (L.b_len + 63) & ~(size_t)63;
-      continue;
-    }
-    if (split_dtype(h->cfg.dtype) && (L.kind == L_CONV || L.kind == L_UPS) &&
-        h->c16 && h->big_tile == 3 && L.M >= 128 &&
-        hfg::c16_supported(L.KT, L.kind == L_UPS, L.M, L.C_in, L.dil)) {
-      // 16x16x32-shape wide layer kernel: A per k-step of two (group, tap) entries
-      L.prec = 1;
-      L.tile = hfg::kC16Tile;
-      L.CK = hfg::kBf16x3Ck;
-      L.m_tiles = (L.M + hfg::kC16MT - 1) / hfg::kC16MT;
-      L.n_chunks = (L.C_in + 15) / 16 * L.KT / 2;  // k-steps (even group count)
-      L.w_off = off;
-      L.w_len = (size_t)L.m_tiles * L.n_chunks * 2 * hfg::kC16MT * 32 / 2;  // bf16 pairs
-      off += (L.w_len + 63) & ~(size_t)63;
-      L.b_off = off;
-      L.b_len = (size_t)L.m_tiles * hfg::kC16MT;
-      off += (L.b_len + 63) & ~(size_t)63;
-      continue;
-    }
-    if (split_dtype(h->cfg.dtype) && (L.kind == L_CONV || L.kind == L_UPS) &&
         hfg::bf16x3_tile_for_rows(L.M) >= 0 && hfg::bf16x3_supported(L.KT, L.dil)) {
       // split-precision path: chunk = 16 channels x TPC taps
-      L.tile = hfg::bf16x3_tile_for_rows(L.M, h->big_tile == hfg::kWsTile ? 3 : h->big_tile);
+      L.tile = hfg::bf16x3_tile_for_rows(L.M, h->big_tile);
       // tile 3 with the A fragments in registers (same packing): layer convs whose tap
       // count has a compile-time instance, whole 16-channel groups
       if (h->areg && L.tile == 3 && L.kind == L_CONV && L.C_in % 16 == 0 &&
@@ -645,56 +628,6 @@ void pack_gemm_weights(const Layer& L, F wt, float* dst) {
 //         + lane*8 + e
 //   row = mt*MT + wave_m*32*WM + wm*32 + (lane & 31), ci = g*16 + 8*(lane >> 5) + e,
 //   tap = tg*TPC + jj; plane 0 = bf16(w), plane 1 = bf16(w - hi).
-// A stream of conv_ws_bf16x3 (conv_ws_bf16x3.hip), in bf16 elements:
-//   idx = (((((((mt*2 + wave_m)*n_g + g)*KT + tap)*2 + wm)*2 + plane)*64 + lane)*8 + e
-//   row = mt*128 + wave_m*64 + wm*32 + (lane & 31), ci = g*16 + 8*(lane >> 5) + e.
-template <typename F>
-void pack_ws(const Layer& L, F wt, uint16_t* dst) {
-  const int n_g = L.n_chunks;
-  size_t idx = 0;
-  for (int mt = 0; mt < L.m_tiles; ++mt)
-    for (int wv = 0; wv < 2; ++wv)
-      for (int g = 0; g < n_g; ++g)
-        for (int tap = 0; tap < L.KT; ++tap)
-          for (int wm = 0; wm < 2; ++wm)
-          for (int plane = 0; plane < 2; ++plane)
-            for (int lane = 0; lane < 64; ++lane)
-              for (int e = 0; e < 8; ++e) {
-                const int row = mt * hfg::kWsMT + wv * 64 + wm * 32 + (lane & 31);
-                const int ci = g * 16 + 8 * (lane >> 5) + e;
-                float v = 0.f;
-                if (row < L.M && ci < L.C_in) v = wt(row, ci, tap);
-                const uint16_t hi = f2bf(v);
-                dst[idx++] = plane == 0 ? hi : f2bf(v - bf2f(hi));
-              }
-}
-
-// A stream of conv16_bf16x3 (conv16_bf16x3.hip), in bf16 elements, per k-step s:
-//   idx = ((((((mt*P + s)*2 + plane)*2 + wave_m)*4 + i)*64 + lane)*8 + e
-//   row = mt*128 + wave_m*64 + i*16 + (lane & 15); entry f = 2s + (lane >> 5),
-//   g = f / KT, tap = f % KT, ci = g*16 + 8*((lane >> 4) & 1) + e.
-template <typename F>
-void pack_c16(const Layer& L, F wt, uint16_t* dst) {
-  const int P = L.n_chunks, KT = L.KT;
-  size_t idx = 0;
-  for (int mt = 0; mt < L.m_tiles; ++mt)
-    for (int s = 0; s < P; ++s)
-      for (int plane = 0; plane < 2; ++plane)
-        for (int wv = 0; wv < 2; ++wv)
-          for (int i = 0; i < 4; ++i)
-            for (int lane = 0; lane < 64; ++lane)
-              for (int e = 0; e < 8; ++e) {
-                const int row = mt * hfg::kC16MT + wv * 64 + i * 16 + (lane & 15);
-                const int f = 2 * s + (lane >> 5);
-                const int g = f / KT, tap = f % KT;
-                const int ci = g * 16 + 8 * ((lane >> 4) & 1) + e;
-                float v = 0.f;
-                if (row < L.M && ci < L.C_in) v = wt(row, ci, tap);
-                const uint16_t hi = f2bf(v);
-                dst[idx++] = plane == 0 ? hi : f2bf(v - bf2f(hi));
-              }
-}
-
 template <typename F>
 void pack_bf16x3(const Layer& L, F wt, uint16_t* dst) {
   const hfg::Bf16x3Cfg& t = hfg::kBf16x3Tiles[L.tile];
@@ -784,42 +717,6 @@ void pack_layer(hfg_handle* h, const Layer& L) {
   if (L.kind == L_POST) {
     std::memcpy(dst, w, sizeof(float) * L.C_in * 7);  // [1][C][7]
     bdst[0] = Bp.data[0];
-    return;
-  }
-  if (L.tile == hfg::kC16Tile) {
-    const int cin = L.C_in, k = L.k, s = L.s, Q = L.KT, cout = L.C_out;
-    if (L.kind == L_CONV)
-      pack_c16(L, [&](int row, int ci, int j) { return w[((size_t)row * cin + ci) * k + j]; },
-               reinterpret_cast<uint16_t*>(dst));
-    else
-      pack_c16(L,
-               [&](int row, int ci, int jj) {
-                 const int co = row / s, r = row % s;
-                 const int kidx = r + s * (Q - 1 - jj);
-                 return kidx < k ? w[((size_t)ci * cout + co) * k + kidx] : 0.f;
-               },
-               reinterpret_cast<uint16_t*>(dst));
-    for (size_t m = 0; m < L.b_len; ++m)
-      bdst[m] = m < (size_t)L.M ? Bp.data[L.kind == L_CONV ? m : m / s] : 0.f;
-    return;
-  }
-  if (L.kind == L_CONV && L.tile == hfg::kWsTile) {
-    const int cin = L.C_in, k = L.k;
-    pack_ws(L, [&](int row, int ci, int j) { return w[((size_t)row * cin + ci) * k + j]; },
-            reinterpret_cast<uint16_t*>(dst));
-    for (size_t m = 0; m < L.b_len; ++m) bdst[m] = m < (size_t)L.M ? Bp.data[m] : 0.f;
-    return;
-  }
-  if (L.kind == L_UPS && L.tile == hfg::kWsTile) {
-    const int s = L.s, Q = L.KT, k = L.k, cout = L.C_out;
-    pack_ws(L,
-            [&](int row, int ci, int jj) {
-              const int co = row / s, r = row % s;
-              const int kidx = r + s * (Q - 1 - jj);
-              return kidx < k ? w[((size_t)ci * cout + co) * k + kidx] : 0.f;
-            },
-            reinterpret_cast<uint16_t*>(dst));
-    for (size_t m = 0; m < L.b_len; ++m) bdst[m] = m < (size_t)L.M ? Bp.data[m / s] : 0.f;
     return;
   }
   if (L.prec == 1 && (L.kind == L_CONV || L.kind == L_UPS)) {
@@ -1036,8 +933,7 @@ int pick_tile(const hfg_handle* h, const Layer& L, hfg::ConvParams& p, int64_t n
               int conc, int& n_tiles, int& m_tiles) {
   int tile = L.tile;
   m_tiles = L.m_tiles;
-  if (L.prec != 1 || L.tile_s < 0 || L.tile == hfg::kWsTile || L.tile == hfg::kC16Tile ||
-      h->small_tile == 0)
+  if (L.prec != 1 || L.tile_s < 0 || h->small_tile == 0)
     return tile;
   // conc: the grids of that many concurrent launches share the chip
   const bool small =
@@ -1083,10 +979,7 @@ int run_conv(hfg_handle* h, Launcher& ln, const Layer& L, const float* x, int64_
   p.n_chunks = L.n_chunks;
   p.dbg = h->dbg_flags;
   p.epi_lds = h->epi_lds;
-  const int ntile = L.tile == hfg::kWsTile    ? hfg::kWsNT
-                    : L.tile == hfg::kC16Tile ? hfg::kC16NT
-                    : L.prec == 1             ? hfg::kBf16x3Tiles[L.tile].NTILE()
-                                              : kTiles[L.tile].NTILE();
+  const int ntile = L.prec == 1 ? hfg::kBf16x3Tiles[L.tile].NTILE() : kTiles[L.tile].NTILE();
   int n_tiles = (int)((Lt + ntile - 1) / ntile), m_tiles = L.m_tiles;
   const int tile = pick_tile(h, L, p, Lt, B, ln.conc, n_tiles, m_tiles);
   const double flop = 2.0 * L.C_out * L.C_in * L.k * (double)Lt * B;
@@ -1095,13 +988,7 @@ int run_conv(hfg_handle* h, Launcher& ln, const Layer& L, const float* x, int64_
   if (mrf && (mrf_mode & 1)) bytes += 4.0 * B * Lt * L.C_out;
   const char* name = nullptr;
   ln.begin(flop, bytes);
-  hipError_t e = L.tile == hfg::kWsTile
-                     ? hfg::launch_conv_ws_bf16x3(L.KT, false, p, n_tiles, L.m_tiles, (int)B,
-                                                  ln.stream, &name)
-                 : L.tile == hfg::kC16Tile
-                     ? hfg::launch_conv16_bf16x3(L.KT, false, p, n_tiles, L.m_tiles, (int)B,
-                                                 ln.stream, &name)
-                 : L.prec == 1
+  hipError_t e = L.prec == 1
                      ? hfg::launch_conv_bf16x3(tile, L.KT, false, h->np, p, n_tiles, m_tiles, (int)B,
                                                ln.stream, &name)
                      : hfg::launch_conv((TileId)L.tile, L.KT, false, p, n_tiles, L.m_tiles,
@@ -1192,23 +1079,14 @@ int run_ups(hfg_handle* h, Launcher& ln, const Layer& L, const float* x, int64_t
   p.L_out = (int)Lout;
   p.n_chunks = L.n_chunks;
   p.dbg = h->dbg_flags;
-  const int ntile = L.tile == hfg::kWsTile    ? hfg::kWsNT
-                    : L.tile == hfg::kC16Tile ? hfg::kC16NT
-                    : L.prec == 1             ? hfg::kBf16x3Tiles[L.tile].NTILE()
-                                              : kTiles[L.tile].NTILE();
+  const int ntile = L.prec == 1 ? hfg::kBf16x3Tiles[L.tile].NTILE() : kTiles[L.tile].NTILE();
   int n_tiles = (p.N + ntile - 1) / ntile, m_tiles = L.m_tiles;
   const int tile = pick_tile(h, L, p, p.N, B, ln.conc, n_tiles, m_tiles);
   const double flop = 2.0 * L.C_in * L.C_out * L.k * (double)Lin * B;
   const double bytes = 4.0 * B * (L.C_in * Lin + L.C_out * Lout) + 4.0 * L.C_in * L.C_out * L.k;
   const char* name = nullptr;
   ln.begin(flop, bytes);
-  hipError_t e = L.tile == hfg::kWsTile
-                     ? hfg::launch_conv_ws_bf16x3(L.KT, true, p, n_tiles, L.m_tiles, (int)B,
-                                                  ln.stream, &name)
-                 : L.tile == hfg::kC16Tile
-                     ? hfg::launch_conv16_bf16x3(L.KT, true, p, n_tiles, L.m_tiles, (int)B,
-                                                 ln.stream, &name)
-                 : L.prec == 1
+  hipError_t e = L.prec == 1
                      ? hfg::launch_conv_bf16x3(tile, L.KT, true, h->np, p, n_tiles, m_tiles, (int)B,
                                                ln.stream, &name)
                      : hfg::launch_conv((TileId)L.tile, L.KT, true, p, n_tiles, L.m_tiles, (int)B,
@@ -1541,7 +1419,6 @@ int create_impl(const hfg_config* cfg, bool mrf_only, int device, hfg_handle** o
   if (const char* bt = getenv("HFG_BF16X3_BIGTILE")) {
     const int v = atoi(bt);
     if (v == 0 || v == 3) h->big_tile = v;
-    if (v == 4) h->big_tile = hfg::kWsTile;
   }
   if (const char* fe = getenv("HFG_FUSED_RB")) h->use_fused_rb = atoi(fe) != 0;
   if (const char* me = getenv("HFG_MFMA16")) h->mfma16 = atoi(me) != 0;
@@ -1552,7 +1429,6 @@ int create_impl(const hfg_config* cfg, bool mrf_only, int device, hfg_handle** o
   if (const char* us = getenv("HFG_UPS_SWIZZLE")) h->ups_swizzle = atoi(us);
   if (const char* el = getenv("HFG_EPI_LDS")) h->epi_lds = atoi(el);
   if (const char* ar = getenv("HFG_AREG")) h->areg = atoi(ar) != 0;
-  if (const char* ce = getenv("HFG_C16")) h->c16 = atoi(ce) != 0;
   if (const char* se = getenv("HFG_SPLIT")) h->split = atoi(se);
   if (const char* sm = getenv("HFG_SPLIT_MIN")) h->split_min_frames = atoll(sm);
   if (const char* rn = getenv("HFG_RB64_NARROW")) h->rb64_narrow = atoi(rn) != 0;
@@ -1566,7 +1442,6 @@ int create_impl(const hfg_config* cfg, bool mrf_only, int device, hfg_handle** o
     // bf16-valued weights: their lo plane is zero, the kernels skip lo(w) * hi(x) (NP 2
     // instances exist for the default tiles and the whole-ResBlock / thin kernels)
     h->np = 2;
-    h->c16 = false;
     if (h->big_tile != 3) h->big_tile = 3;
   }
   rc = build_layers(h);
@@ -1585,7 +1460,14 @@ int create_impl(const hfg_config* cfg, bool mrf_only, int device, hfg_handle** o
 // ============================================================================
 extern "C" {
 
-const char* hfg_version(void) { return "hifigan_hip 0.2.0 gfx950 fp32-mfma bf16x3-mfma"; }
+#ifndef HFG_SRC_HASH
+#define HFG_SRC_HASH "unknown"
+#endif
+// "... src:<16 hex>": sha256 of the build inputs (csrc/, include/, flags), computed by
+// build.py and compiled in, so a loaded binary can be matched to its source tree
+const char* hfg_version(void) {
+  return "hifigan_hip 0.3.0 gfx950 fp32-mfma bf16x3-mfma src:" HFG_SRC_HASH;
+}
 
 const char* hfg_last_error(void) { return g_err.c_str(); }
 
@@ -1985,8 +1867,6 @@ int hfg_debug_packed_layer(hfg_handle* h, const char* mod, float* out, size_t ca
       info[7] = (int64_t)L.b_len;
       info[8] = L.CK;
       info[9] = L.kind == L_POST ? 0
-                : L.tile == hfg::kWsTile ? hfg::kWsMT
-                : L.tile == hfg::kC16Tile ? hfg::kC16MT
                 : L.prec == 1    ? hfg::kBf16x3Tiles[L.tile].MT()
                                  : kTiles[L.tile].MT();
     }

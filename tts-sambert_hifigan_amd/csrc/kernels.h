@@ -3,9 +3,17 @@
 #pragma once
 
 #include <hip/hip_runtime.h>
+
+#include <mutex>
 #include <stdint.h>
 
 namespace hfg {
+
+// One-time launch setup of a kernel entry, safe across threads and devices:
+// the dynamic-LDS limit is a per-device function attribute, so it is set once per
+// (kernel, device) under a lock; entry names are formatted under the same lock.
+hipError_t ensure_max_lds(const void* fn);
+std::mutex& setup_mutex();
 
 constexpr float kLReluSlope = 0.1f;  // F.leaky_relu(x, 0.1), models/hifigan.py:81,83,244,254
 
@@ -145,32 +153,6 @@ inline bool bf16x3_supported(int kt, int dil) {
 hipError_t launch_conv_bf16x3(int tile, int kt, bool ups, int np, const ConvParams& p,
                               int n_tiles, int m_tiles, int batch, hipStream_t stream,
                               const char** name);
-
-// ---- warp-specialized bf16x3 conv (conv_ws_bf16x3.hip) ----
-// 128 x 256 block tile, 4 consumer waves (64 x 128 each) + 4 producer waves; weights
-// streamed from global memory, packed [m_tile][wave_m][group][tap][wm][plane][lane][8].
-// Selected with tile id kWsTile in the host layer table.
-constexpr int kWsTile = 8;   // tile id (HFG_BF16X3_BIGTILE=4 selects it)
-constexpr int kWsWaves = 8;
-constexpr int kWsMT = 128;
-constexpr int kWsNT = 256;
-bool ws_supported(int kt, bool ups, int M, int dil);
-size_t ws_lds_bytes(int kt, int dil);
-hipError_t launch_conv_ws_bf16x3(int kt, bool ups, const ConvParams& p, int n_tiles, int m_tiles,
-                                 int batch, hipStream_t stream, const char** name);
-
-// ---- 16x16x32-shape wide layer kernel (conv16_bf16x3.hip) ----
-// 128 x 256 block tile, 4 waves of 64 x 128; K walked as (channel group, tap) entries two
-// per k-step; A packed per k-step [m_tile][step][plane][wave_m][row tile][lane][8].
-// Needs an even channel-group count and (KT-1)*dil <= kC16MaxHalo.
-constexpr int kC16Tile = 9;  // tile id
-constexpr int kC16MT = 128;
-constexpr int kC16NT = 256;
-constexpr int kC16MaxHalo = 128;
-bool c16_supported(int kt, bool ups, int M, int C_in, int dil);
-size_t c16_lds_bytes(int kt, int dil);
-hipError_t launch_conv16_bf16x3(int kt, bool ups, const ConvParams& p, int n_tiles, int m_tiles,
-                                int batch, hipStream_t stream, const char** name);
 
 // ---- whole ResBlock per launch (resblock_bf16x3.hip) ----
 // All 2*n_dil convs of one ResBlock of a C in {32, 64} stage on a window of

@@ -29,6 +29,8 @@
 // every operand write — the zero padding of each reference conv input.
 #include <hip/hip_runtime.h>
 
+#include <mutex>
+
 #include <cstdio>
 
 #include "bf16x3_common.h"
@@ -198,12 +200,11 @@ typedef void (*ThinFn)(const ThinParams);
 struct EntryThin {
   int C, ncol, nt, wpe;
   ThinFn fn;
-  bool attr;
   char name[48];
 };
 
 #define HFGTHIN_ENTRY(C_, NCOL_, NT_, WPE_) \
-  { C_, NCOL_, NT_, WPE_, mrf_thin<C_, NCOL_, NT_, WPE_>, false, {0} }
+  { C_, NCOL_, NT_, WPE_, mrf_thin<C_, NCOL_, NT_, WPE_>, {0} }
 
 EntryThin g_entriesThin[] = {HFGTHIN_ENTRY(16, 2, 256, 3), HFGTHIN_ENTRY(8, 4, 256, 3),
                              HFGTHIN_ENTRY(4, 8, 256, 3)};
@@ -243,14 +244,13 @@ hipError_t launch_mrf_thin(int C, const ThinParams& p, int batch, hipStream_t st
   }
   const size_t lds = thin_lds_bytes(C);
   if (lds > 160 * 1024) return hipErrorInvalidValue;
-  if (!e->attr) {
-    hipError_t err = hipFuncSetAttribute(reinterpret_cast<const void*>(e->fn),
-                                         hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    if (err != hipSuccess) return err;
-    e->attr = true;
+  if (hipError_t err = ensure_max_lds(reinterpret_cast<const void*>(e->fn)))
+    return err;
+  {
+    std::lock_guard<std::mutex> lk(setup_mutex());
+    if (!e->name[0]) snprintf(e->name, sizeof(e->name), "mrf_thin<%d, %d, %d, %d>", e->C, e->ncol, e->nt,
+                               e->wpe);
   }
-  if (!e->name[0]) snprintf(e->name, sizeof(e->name), "mrf_thin<%d, %d, %d, %d>", e->C, e->ncol, e->nt,
-                             e->wpe);
   if (name) *name = e->name;
   const int n_tiles = (p.L + p.W - 1) / p.W;
   e->fn<<<dim3(n_tiles, batch), dim3(e->nt), lds, stream>>>(p);

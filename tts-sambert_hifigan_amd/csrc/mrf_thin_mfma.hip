@@ -31,6 +31,8 @@
 // (uniform across the block) into registers one conv ahead.
 #include <hip/hip_runtime.h>
 
+#include <mutex>
+
 #include <cstdio>
 
 #include "bf16x3_common.h"
@@ -255,13 +257,12 @@ typedef void (*ThinMfmaFn)(const ThinParams);
 struct EntryThinMfma {
   int C, np;
   ThinMfmaFn fn;
-  bool attr;
   char name[40];
 };
 
-EntryThinMfma g_entriesThinMfma[] = {{16, 3, mrf_thin_mfma<16, 3>, false, {0}},
-                                     {8, 3, mrf_thin_mfma<8, 3>, false, {0}},
-                                     {16, 2, mrf_thin_mfma<16, 2>, false, {0}}};
+EntryThinMfma g_entriesThinMfma[] = {{16, 3, mrf_thin_mfma<16, 3>, {0}},
+                                     {8, 3, mrf_thin_mfma<8, 3>, {0}},
+                                     {16, 2, mrf_thin_mfma<16, 2>, {0}}};
 
 EntryThinMfma* find_thin_mfma(int C, int np = 3) {
   for (auto& e : g_entriesThinMfma)
@@ -297,13 +298,12 @@ hipError_t launch_mrf_thin_mfma(int C, int np, const ThinParams& p, int batch,
         return hipErrorInvalidValue;
   }
   const size_t lds = thin_mfma_lds_bytes(C);
-  if (!e->attr) {
-    hipError_t err = hipFuncSetAttribute(reinterpret_cast<const void*>(e->fn),
-                                         hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    if (err != hipSuccess) return err;
-    e->attr = true;
+  if (hipError_t err = ensure_max_lds(reinterpret_cast<const void*>(e->fn)))
+    return err;
+  {
+    std::lock_guard<std::mutex> lk(setup_mutex());
+    if (!e->name[0]) snprintf(e->name, sizeof(e->name), "mrf_thin_mfma<%d, %d>", e->C, e->np);
   }
-  if (!e->name[0]) snprintf(e->name, sizeof(e->name), "mrf_thin_mfma<%d, %d>", e->C, e->np);
   if (name) *name = e->name;
   const int n_tiles = (p.L + p.W - 1) / p.W;
   e->fn<<<dim3(n_tiles, batch), dim3(256), lds, stream>>>(p);

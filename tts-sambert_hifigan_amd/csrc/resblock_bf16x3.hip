@@ -31,6 +31,8 @@
 // passes per dilation for the layer-per-launch schedule.
 #include <hip/hip_runtime.h>
 
+#include <mutex>
+
 #include <cstdio>
 
 #include "bf16x3_common.h"
@@ -299,12 +301,11 @@ typedef void (*RbFn)(const RbParams);
 struct EntryRb {
   int kt, waves_m, waves_n, np;
   RbFn fn;
-  bool attr;
   char name[64];
 };
 
 #define HFGRB_ENTRY(KT, WMS, WNS, NP) \
-  { KT, WMS, WNS, NP, resblock_bf16x3<KT, WMS, WNS, NP>, false, {0} }
+  { KT, WMS, WNS, NP, resblock_bf16x3<KT, WMS, WNS, NP>, {0} }
 #define HFGRB_KTS(WMS, WNS, NP)                                                                 \
   HFGRB_ENTRY(3, WMS, WNS, NP), HFGRB_ENTRY(5, WMS, WNS, NP), HFGRB_ENTRY(7, WMS, WNS, NP), \
       HFGRB_ENTRY(11, WMS, WNS, NP)
@@ -344,17 +345,16 @@ hipError_t launch_resblock_bf16x3(int C, int waves_n, int kt, int np, const RbPa
   if (p.W <= 0 || p.halo < 0 || p.W + 2 * p.halo > nwin) return hipErrorInvalidValue;
   for (int i = 0; i < p.n_conv; ++i)
     if (p.dil[i] < 1 || (kt - 1) / 2 * p.dil[i] > rb_marg(C, waves_n)) return hipErrorInvalidValue;
-  if (!e->name[0])
-    snprintf(e->name, sizeof(e->name), "resblock_bf16x3<%d, %d, %d, %d>", e->kt, e->waves_m,
-             e->waves_n, e->np);
+  {
+    std::lock_guard<std::mutex> lk(setup_mutex());
+    if (!e->name[0])
+      snprintf(e->name, sizeof(e->name), "resblock_bf16x3<%d, %d, %d, %d>", e->kt, e->waves_m,
+               e->waves_n, e->np);
+  }
   const size_t lds = rb_lds_bytes(C, waves_n, p.n_conv);
   if (lds > 160 * 1024) return hipErrorInvalidValue;
-  if (!e->attr) {
-    hipError_t err = hipFuncSetAttribute(reinterpret_cast<const void*>(e->fn),
-                                         hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    if (err != hipSuccess) return err;
-    e->attr = true;
-  }
+  if (hipError_t err = ensure_max_lds(reinterpret_cast<const void*>(e->fn)))
+    return err;
   if (name) *name = e->name;
   const int n_tiles = (p.L + p.W - 1) / p.W;
   e->fn<<<dim3(n_tiles, batch), dim3(64 * wm * waves_n), lds, stream>>>(p);

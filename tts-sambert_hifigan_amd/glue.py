@@ -15,7 +15,7 @@ here on the same HIP kernels:
 """
 from __future__ import annotations
 
-from typing import List, Optional, Sequence
+from typing import Dict, List, Optional, Sequence
 
 import torch
 
@@ -43,51 +43,161 @@ def vocode_list(gen, mels: Sequence[torch.Tensor]) -> List[torch.Tensor]:
 
 
 class StreamingVocoder:
-    """Chunked vocoding of a growing mel stream for ONE utterance.
+    """Chunked vocoding of growing mel streams with bounded state (SURVEY.md §8(f) 3;
+    the reference's Requirement 18, ``.kiro/specs/tts-sam-bert-hifigan/requirements.md:
+    211-220``, and its unbuilt ``StreamingBuffer``, ``tasks.md:362-368``).
 
-    ``push(frames [n_mels, t])`` returns the audio that is final so far;
-    ``flush()`` returns the rest.  A chunk of ``chunk_frames`` is emitted once
-    ``context`` future frames exist; it is computed from the frames
-    ``[start - context, end + context)`` and cropped, so the output is identical
-    to ``gen(full_mel)`` (context defaults to gen.receptive_field_frames()).
-    Needs an exact-upsampling config (output length = frames × hop).
+    A chunk of ``chunk_frames`` new frames is emitted once ``context`` future frames
+    exist; it is computed from the frames ``[start - context, end + context)`` and
+    cropped, so the concatenated audio of a stream is BITWISE the one-shot
+    ``gen(full_mel)`` (``context`` defaults to ``gen.receptive_field_frames()``, beyond
+    which an output sample does not depend on the input: no overlap-add or crossfade is
+    needed, the seams are exact).  Needs an exact-upsampling config (out = T x hop).
+
+    Bounded state: a stream keeps only the frames ``[emitted - context, received)`` in
+    a per-stream buffer of fixed capacity (``chunk + 2 context`` + the largest push so
+    far), so memory and per-push cost do not grow with the stream's length.
+
+    Several streams (``n_streams``) share each forward: :meth:`feed` appends frames
+    without computing, :meth:`step` vocodes the next ready chunk of EVERY stream as one
+    ragged batch (per-item lengths, ``hfg_forward_ex``; each item equals its window
+    run alone, so batching changes no sample), :meth:`finish` marks a stream's end so
+    its tail is emitted by the following steps.  :meth:`push` / :meth:`flush` are the
+    one-stream convenience (feed, then step until nothing is ready).  With
+    ``debug_shapes`` (default: the generator's, i.e. ``DEBUG_SHAPES=1``) every chunk
+    prints its shapes (Requirement 18.4).
     """
 
-    def __init__(self, gen, chunk_frames: int = 64, context: Optional[int] = None):
+    def __init__(self, gen, chunk_frames: int = 64, context: Optional[int] = None,
+                 n_streams: int = 1, debug_shapes: Optional[bool] = None):
         self.gen = gen
         self.hop = gen.output_length(2) - gen.output_length(1)
         if gen.output_length(7) != 7 * self.hop:
             raise ValueError("streaming needs exact upsampling (out_len = T * hop)")
+        if chunk_frames < 1 or n_streams < 1:
+            raise ValueError("chunk_frames and n_streams must be >= 1")
         self.chunk = int(chunk_frames)
         self.ctx = int(context) if context is not None else gen.receptive_field_frames()
-        self.buf: Optional[torch.Tensor] = None  # all frames received [n_mels, T]
-        self.emitted = 0                         # frames whose audio was returned
+        self.n_streams = int(n_streams)
+        self.debug_shapes = (getattr(gen, "debug_shapes", False) if debug_shapes is None
+                             else bool(debug_shapes))
+        self._buf: List[Optional[torch.Tensor]] = [None] * self.n_streams  # [n_mels, cap]
+        self._start = [0] * self.n_streams     # absolute frame index of _buf[s][:, 0]
+        self._fill = [0] * self.n_streams      # valid columns of _buf[s]
+        self._done = [False] * self.n_streams
+        self._emitted = [0] * self.n_streams   # frames whose audio was returned
+        self.chunks_run = 0
 
-    def _run(self, a: int, b: int, end: int) -> torch.Tensor:
-        lo, hi = max(0, a - self.ctx), min(end, b + self.ctx)
-        with torch.no_grad():
-            wav = self.gen(self.buf[None, :, lo:hi].contiguous())
-        return wav[0, 0, (a - lo) * self.hop:(b - lo) * self.hop]
+    # -- state -------------------------------------------------------------------------
+    @property
+    def emitted(self) -> int:
+        return self._emitted[0]
 
-    def push(self, frames: torch.Tensor) -> torch.Tensor:
+    def received(self, stream: int = 0) -> int:
+        return self._start[stream] + self._fill[stream]
+
+    def buffered_frames(self, stream: int = 0) -> int:
+        """Frames currently held for `stream` (bounded: <= chunk + 2 context + a push)."""
+        return self._fill[stream]
+
+    def capacity(self, stream: int = 0) -> int:
+        b = self._buf[stream]
+        return 0 if b is None else b.shape[1]
+
+    def feed(self, frames: torch.Tensor, stream: int = 0) -> None:
+        """Append mel frames [n_mels, t] (or [1, n_mels, t]) to `stream`; no compute."""
         if frames.dim() == 3:
             frames = frames[0]
-        self.buf = frames if self.buf is None else torch.cat([self.buf, frames], dim=1)
-        T = self.buf.shape[1]
-        out = []
-        while T - self.emitted >= self.chunk + self.ctx:
-            a, b = self.emitted, self.emitted + self.chunk
-            out.append(self._run(a, b, T))
-            self.emitted = b
-        return torch.cat(out) if out else self.buf.new_zeros(0)
+        if self._done[stream]:
+            raise RuntimeError(f"stream {stream} was finished")
+        t = frames.shape[1]
+        if t == 0:
+            return
+        buf, fill = self._buf[stream], self._fill[stream]
+        need = fill + t
+        if buf is None or need > buf.shape[1] or buf.device != frames.device:
+            cap = max(need, self.chunk + 2 * self.ctx + t)
+            nb = torch.empty(frames.shape[0], cap, dtype=torch.float32, device=frames.device)
+            if buf is not None and fill:
+                nb[:, :fill].copy_(buf[:, :fill])
+            self._buf[stream] = buf = nb
+        buf[:, fill:need].copy_(frames)
+        self._fill[stream] = need
 
-    def flush(self) -> torch.Tensor:
-        if self.buf is None:
-            return torch.zeros(0)
-        T = self.buf.shape[1]
+    def finish(self, stream: int = 0) -> None:
+        """No more frames for `stream`: its remaining audio is emitted by later steps."""
+        self._done[stream] = True
+
+    def _window(self, s: int):
+        """(a, b, lo, hi) absolute frames of `s`'s next ready chunk, or None."""
+        T, a = self.received(s), self._emitted[s]
+        if self._done[s]:
+            if a >= T:
+                return None
+            b = min(T, a + self.chunk)
+        else:
+            if T - a < self.chunk + self.ctx:
+                return None
+            b = a + self.chunk
+        return a, b, max(0, a - self.ctx), min(T, b + self.ctx)
+
+    def _trim(self, s: int) -> None:
+        """Drop frames no future chunk reads: keep [emitted - ctx, received)."""
+        keep_from = max(self._start[s], self._emitted[s] - self.ctx)
+        drop = keep_from - self._start[s]
+        if drop > 0:
+            buf, fill = self._buf[s], self._fill[s]
+            rest = fill - drop
+            if rest > 0:
+                # regions overlap when rest > drop: clone the source first
+                buf[:, :rest].copy_(buf[:, drop:fill].clone() if rest > drop else buf[:, drop:fill])
+            self._start[s] = keep_from
+            self._fill[s] = rest
+
+    def step(self, streams: Optional[Sequence[int]] = None) -> Dict[int, torch.Tensor]:
+        """One batched forward over every stream (of `streams`, default all) with a ready
+        chunk -> {stream: audio of that chunk}."""
+        cand = range(self.n_streams) if streams is None else streams
+        ready = [(s, w) for s in cand if (w := self._window(s)) is not None]
+        if not ready:
+            return {}
+        lens = [hi - lo for _, (a, b, lo, hi) in ready]
+        W = max(lens)
+        dev = self._buf[ready[0][0]].device
+        n_mels = self._buf[ready[0][0]].shape[0]
+        mel = torch.zeros(len(ready), n_mels, W, dtype=torch.float32, device=dev)
+        for i, (s, (a, b, lo, hi)) in enumerate(ready):
+            off = lo - self._start[s]
+            mel[i, :, :hi - lo].copy_(self._buf[s][:, off:off + hi - lo])
+        with torch.no_grad():
+            wav = self.gen(mel, lengths=None if min(lens) == W else lens)
+        out = {}
+        for i, (s, (a, b, lo, hi)) in enumerate(ready):
+            out[s] = wav[i, 0, (a - lo) * self.hop:(b - lo) * self.hop]
+            if self.debug_shapes:
+                print(f"[StreamingVocoder] stream {s} chunk {self.chunks_run}: frames [{a}, {b}) "
+                      f"context [{lo}, {hi}) mel {tuple(mel[i:i + 1, :, :hi - lo].shape)} -> "
+                      f"wav {tuple(out[s].shape)}")
+            self._emitted[s] = b
+            self._trim(s)
+        self.chunks_run += 1
+        return out
+
+    def push(self, frames: torch.Tensor, stream: int = 0) -> torch.Tensor:
+        """Feed `frames` to `stream` and return all of its audio that is final now."""
+        self.feed(frames, stream)
+        return self._drain(stream)
+
+    def flush(self, stream: int = 0) -> torch.Tensor:
+        """End `stream` and return the rest of its audio."""
+        self.finish(stream)
+        return self._drain(stream)
+
+    def _drain(self, stream: int) -> torch.Tensor:
         out = []
-        while self.emitted < T:
-            a, b = self.emitted, min(T, self.emitted + self.chunk)
-            out.append(self._run(a, b, T))
-            self.emitted = b
-        return torch.cat(out) if out else self.buf.new_zeros(0)
+        while self._window(stream) is not None:
+            out.append(self.step([stream])[stream])
+        if out:
+            return torch.cat(out)
+        b = self._buf[stream]
+        return torch.zeros(0, device=b.device if b is not None else None)

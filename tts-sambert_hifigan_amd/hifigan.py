@@ -25,12 +25,27 @@ autograd; a CPU input or an input that requires grad raises.
 from __future__ import annotations
 
 import os
+import weakref
 from typing import Dict, List, Tuple
 
 import torch
 import torch.nn as nn
 
 from . import _lib
+
+
+def _on_param_registered(module, name, param):
+    """Global nn.Module parameter-registration hook: a conv owned by a HIP module got a
+    new parameter object (replacement, weight norm applied / removed) -> its owners
+    re-read their parameter list and re-pack before the next forward."""
+    owners = module.__dict__.get("_hfg_owners")
+    if owners:
+        for o in list(owners):
+            o.refresh_weights()
+    return None
+
+
+nn.modules.module.register_module_parameter_registration_hook(_on_param_registered)
 
 
 def get_padding(kernel_size: int, dilation: int = 1) -> int:
@@ -45,22 +60,22 @@ class _HipWeights(nn.Module):
     containers; a handle per device holds them packed in the kernels' layout.  They
     are re-packed before a forward when any parameter was replaced, resized or
     moved (data_ptr / shape), bumped its autograd version (in-place ops, ``copy_``
-    under no_grad), after ``load_state_dict`` / ``.to()`` / ``refresh_weights()``,
-    and — with ``verify_weights`` (default) — when a device-side content hash of
-    the parameters (``hfg_checksum32``) differs from the one at the last commit,
-    which catches edits through ``param.data`` that leave the version counter
-    untouched.  The hash costs one small D2H read (a stream sync) per forward; it
-    is skipped while a hipGraph is being captured.  Set ``verify_weights = False``
-    for fully asynchronous launches and call ``refresh_weights()`` after editing
-    weights through ``.data``.
+    under no_grad), and after ``load_state_dict`` / ``.to()`` / ``refresh_weights()``.
+    The check is host-side bookkeeping only: a forward launches asynchronously, with
+    no host sync.  An edit through ``param.data`` leaves the version counter untouched:
+    call ``refresh_weights()`` after one, or set ``verify_weights = True`` (opt-in) to
+    compare a device-side content hash of the parameters (``hfg_checksum32``) before
+    every forward — one small D2H read, i.e. a stream sync per forward (skipped while a
+    hipGraph is being captured).
     """
 
-    verify_weights = True
+    verify_weights = False
 
     def _hip_setup(self, precision: str):
         self._hfg_handles: Dict[int, _lib.Handle] = {}
         self._hfg_fingerprint: Dict[int, tuple] = {}
         self._hfg_checksum: Dict[int, torch.Tensor] = {}
+        self._hfg_items = None  # cached (key, tensor) list, rebuilt after any invalidation
         self.precision = precision
         self.register_load_state_dict_post_hook(_HipWeights._after_load)
 
@@ -73,12 +88,35 @@ class _HipWeights(nn.Module):
         """Force a re-pack of the parameters before the next forward."""
         self._hfg_fingerprint = {}
         self._hfg_checksum = {}
+        self._hfg_items = None
         return self
 
     def _apply(self, fn, *args, **kwargs):
         out = super()._apply(fn, *args, **kwargs)
+        # parameters moved / converted (possibly of a submodule shared with another owner)
+        for m in self.modules():
+            for o in list(getattr(m, "_hfg_owners", ())):
+                o.refresh_weights()
         self.refresh_weights()
         return out
+
+    def _items(self):
+        """The (key, tensor) list, cached: walking the module tree costs ~0.6 ms for V1,
+        more than a C1 forward's host budget.  A parameter (re)registered on any conv of
+        this module (``conv.weight = Parameter(..)``, weight norm applied / removed) fires
+        the registration hook below, which drops the cache."""
+        items = self._hfg_items
+        if items is None:
+            items = list(self._hip_weight_items())
+            for m in self.modules():
+                if isinstance(m, (nn.Conv1d, nn.ConvTranspose1d)):
+                    owners = m.__dict__.get("_hfg_owners")
+                    if owners is None:
+                        owners = weakref.WeakSet()
+                        m.__dict__["_hfg_owners"] = owners
+                    owners.add(self)
+            self._hfg_items = items
+        return items
 
     # subclasses: (key, tensor) of every parameter in the handle's key space, and the handle
     def _hip_weight_items(self):
@@ -93,13 +131,15 @@ class _HipWeights(nn.Module):
         if h is None:
             h = self._hip_new_handle(idx)
             self._hfg_handles[idx] = h
-        items = list(self._hip_weight_items())
-        fp = tuple((k, t.data_ptr(), t._version, tuple(t.shape), str(t.device)) for k, t in items)
+        items = self._items()
+        # in-place edits bump _version; replaced storage changes data_ptr (shapes and
+        # devices only change with a new storage); one pass, ~50 us for V1's 156 tensors
+        fp = (tuple([t._version for _, t in items]), tuple([t.data_ptr() for _, t in items]))
         stale = self._hfg_fingerprint.get(idx) != fp
-        dev_ts = [t.detach() for _, t in items if t.is_cuda and t.dtype == torch.float32
-                  and t.is_contiguous()]
-        check = (self.verify_weights and dev_ts and
-                 not torch.cuda.is_current_stream_capturing())
+        check = self.verify_weights and not torch.cuda.is_current_stream_capturing()
+        dev_ts = ([t.detach() for _, t in items if t.is_cuda and t.dtype == torch.float32
+                   and t.is_contiguous()] if check else [])
+        check = check and bool(dev_ts)
         cks = None
         if not stale and check:
             cks = _lib.checksum32(dev_ts)
