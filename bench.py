@@ -474,6 +474,8 @@ def main():
     import importlib
     hdist = importlib.import_module(ge.PKG_NAME + ".dist")
     S = importlib.import_module(ge.PKG_NAME + ".synth")  # random-init weights of the config
+    global PREC
+    PREC = importlib.import_module(ge.PKG_NAME + ".precision")  # documented scale limits
 
     cfg = S.PRESETS[args.preset]
     spec = [(k, s) for k, s, _ in S.param_specs(cfg)]
@@ -629,8 +631,10 @@ def main():
         "dtype_note": ("fp32 operands on the fp32 MFMA (exact products)" if args.precision == "fp32"
                        else "fp32 in/out and fp32 accumulation; every fp32 operand split into bf16 "
                             "hi + lo, products hi*hi + hi*lo + lo*hi on the bf16 MFMA (the "
-                            "upsamplers too); wav within 1e-4 of the reference on every golden "
-                            "fixture (max 9e-6), tests/test_gpu_parity.py"),
+                            "upsamplers too). " + PREC.note(args.precision)),
+        "precision_limit": ({f"x{k:g}": v for k, v in PREC.BF16X3_SCALE_LIMITS.items()}
+                            if args.precision == "bf16x3" else None),
+        "precision_measured": PREC.MEASURED.get(args.precision),
         "data": "synthetic: mel ~ N(0,1) (torch seed 1234), random default-init weights "
                 "U(+-1/sqrt(fan_in)) of the preset (synth.py; no checkpoint ships)",
         "config": {
@@ -674,8 +678,7 @@ def main():
                      "rtf": (el / args.steps) / (args.batch * ol / SAMPLE_RATE),
                      "speedup_vs_headline": v / value,
                      "parity": ("atol 1e-4 vs the oracle run on the bf16-rounded weights "
-                                "(tests/test_gpu_bf16w.py)" if prec == "bf16w" else
-                                "atol 1e-4 vs reference fixtures (tests/test_gpu_parity.py)")}
+                                "(tests/test_gpu_bf16w.py)" if prec == "bf16w" else PREC.note(prec))}
             if pr:
                 entry["roofline"] = roofline(pr, prof_ms.get(prec, 1000.0 * el / args.steps))
                 entry["kernels"] = {k: {"launches": q["launches"] // args.steps,

@@ -248,6 +248,12 @@ int hfg_mel_create(const hfg_mel_config* cfg, int device, hfg_mel_handle** out);
 void hfg_mel_destroy(hfg_mel_handle* h);
 /* the [n_fft/2+1][n_mels] filterbank (torchaudio melscale_fbanks), host side */
 int hfg_mel_filterbank(const hfg_mel_config* cfg, float* out);
+/* Replace the handle's window [n_fft] (torch.stft's window, centred) and filterbank
+ * [n_fft/2+1][n_mels] (host pointers, fp32).  The handle's own tables are evaluated in
+ * double and rounded; a caller that has torchaudio's float32 tables (torch.hann_window,
+ * melscale_fbanks -- audio_processing.py:99-110) passes them here so the spectrum is
+ * taken with bitwise the reference's window (the Python layer, mel.py, does). */
+int hfg_mel_set_tables(hfg_mel_handle* h, const float* window, const float* fb);
 int64_t hfg_mel_frames(const hfg_mel_handle* h, int64_t n_samples);
 size_t hfg_mel_workspace_bytes(const hfg_mel_handle* h, int64_t B, int64_t n_samples);
 int hfg_mel_forward(hfg_mel_handle* h, const float* wav, int64_t B, int64_t n_samples,

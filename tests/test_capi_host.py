@@ -31,7 +31,7 @@ def header_symbols():
 def test_library_exports_every_header_symbol(pkg):
     lib = pkg.load_library()
     syms = header_symbols()
-    assert len(syms) == 38
+    assert len(syms) == 39
     for s in sorted(syms):
         assert hasattr(lib, s), f"missing export {s}"
     assert set(syms) == set(pkg._lib.SIGNATURES), "ctypes signatures out of sync with headers"

@@ -2,12 +2,17 @@
 restatement (oracle/mel_torch.py).  PARITY UNPINNED: torchaudio, which the
 reference calls, is absent from this image, so the oracle is a restatement of
 its published algorithm (same torch.stft call, same float32 filterbank code).
-Tolerance (fp32 DFT by direct summation vs pocketfft): |log10 mel - oracle| <= 1e-4
-where the oracle mel >= 1e-2 x its max (the bands that carry the signal: a relative
-power error of ~2e-4; measured <= 3e-5), <= 5e-4 where it is >= 1e-6 x its max
-(measured <= 7e-5), and <= 2e-2 everywhere else (measured <= 6.2e-3) (bins ~60 dB below the peak, where the fp32 summation's absolute error of ~1e-7 of
-the peak power dominates).  The resampler (torchaudio Resample restated in
-oracle/resample_np.py, float64) is checked at 2e-6 x max|x|."""
+
+The device path (csrc/mel_kernels.hip logmel_fft, round 3) is an FFT with the spectrum in
+float64, so it is compared two ways:
+* vs ``log_mel64`` (the same algorithm with a float64 spectrum): |log10 mel - oracle| <=
+  1e-5 on EVERY band, quiet ones included (measured ~1e-6: the float32 output rounding);
+* vs ``log_mel`` (float32 torch.stft, what torchaudio computes): <= 1e-4 where the oracle
+  mel >= 1e-6 x its max (measured <= 7e-5) and <= 2e-2 elsewhere — there the float32 FFT's
+  own absolute error (~1e-7 of the frame energy per bin) dominates, not the device's.
+The DFT-GEMM fallback (HFG_MEL_DFT=1, n_fft not a power of two) keeps the float32 bounds
+of round 2.  The resampler (torchaudio Resample restated in oracle/resample_np.py, float64)
+is checked at 2e-6 x max|x|."""
 import numpy as np
 import pytest
 import torch
@@ -31,14 +36,21 @@ def _signals(n):
     return torch.stack([tone + noise, chirp])
 
 
-def _check(got, ref):
+def _check(got, ref, ref64=None, fft=True):
+    """ref: float32 torch restatement; ref64: the float64-spectrum restatement."""
     strong = ref >= np.log10(1e-2) + ref.max()
     big = ref >= np.log10(1e-6) + ref.max()
     err = (got - ref).abs()
-    print(f"\nlog-mel error: strong {err[strong].max().item():.2e}, "
-          f">=1e-6 {err[big].max().item():.2e}, all {err.max().item():.2e}")
+    msg = (f"\nlog-mel error vs fp32 oracle: strong {err[strong].max().item():.2e}, "
+           f">=1e-6 {err[big].max().item():.2e}, all {err.max().item():.2e}")
+    if ref64 is not None:
+        e64 = (got.double() - ref64).abs().max().item()
+        msg += f"; vs fp64 oracle: all {e64:.2e}"
+        if fft:
+            assert e64 <= 1e-5, e64
+    print(msg)
     assert err[strong].max().item() <= 1e-4, err[strong].max().item()
-    assert err[big].max().item() <= 5e-4, err[big].max().item()
+    assert err[big].max().item() <= (1e-4 if fft else 5e-4), err[big].max().item()
     assert err.max().item() <= 2e-2, err.max().item()
 
 
@@ -52,7 +64,59 @@ def test_mel_vs_restatement(pkg, dev, n):
     got = ext(wav.to(dev)).cpu()
     ref = M.log_mel(wav)
     assert got.shape == ref.shape == (2, 80, n // 256 + 1)
-    _check(got, ref)
+    _check(got, ref, M.log_mel64(wav))
+
+
+def test_mel_quiet_bands_fp64(pkg, dev):
+    """Silence next to loud frames (the verdict's quiet-bin case): a burst of tone + noise,
+    then 1e-4-level noise and exact digital silence.  Every band — down to the 1e-10 floor —
+    within 1e-5 (log10) of the float64-spectrum restatement."""
+    import importlib
+    melmod = importlib.import_module("tts_sambert_hifigan_amd.mel")
+    from oracle import mel_torch as M
+    n = 3 * 22050
+    g = torch.Generator().manual_seed(3)
+    t = torch.arange(n) / 22050.0
+    wav = 0.8 * torch.sin(2 * np.pi * 440.0 * t) + 0.05 * torch.randn(n, generator=g)
+    wav[n // 3:2 * n // 3] = 1e-4 * torch.randn(n // 3, generator=g)
+    wav[2 * n // 3:] = 0.0
+    got = melmod.MelSpectrogram(device=dev)(wav[None].to(dev)).cpu()[0]
+    ref64 = M.log_mel64(wav)
+    e = (got.double() - ref64).abs()
+    quiet = ref64 < ref64.max() - 6.0
+    print(f"\nquiet bands {int(quiet.sum())}: max err {e[quiet].max().item():.2e}; "
+          f"all {e.max().item():.2e}")
+    assert quiet.sum() > 1000
+    assert e.max().item() <= 1e-5
+
+
+@pytest.mark.parametrize("n_fft,hop", [(512, 128), (2048, 512), (256, 64)])
+def test_mel_other_fft_sizes(pkg, dev, n_fft, hop):
+    """Other power-of-two n_fft (radix 8 / 4 / 2 Stockham passes) vs the float64 oracle."""
+    import importlib
+    melmod = importlib.import_module("tts_sambert_hifigan_amd.mel")
+    from oracle import mel_torch as M
+    cfg = dict(M.CONFIG, n_fft=n_fft, hop_length=hop, win_length=n_fft)
+    wav = _signals(7000)
+    got = melmod.MelSpectrogram(n_fft=n_fft, hop_length=hop, win_length=n_fft,
+                                device=dev)(wav.to(dev)).cpu()
+    ref64 = M.log_mel64(wav, cfg)
+    assert got.shape == ref64.shape
+    e = (got.double() - ref64).abs().max().item()
+    print(f"\nn_fft {n_fft} hop {hop}: max err vs fp64 {e:.2e}")
+    assert e <= 1e-5
+
+
+def test_mel_dft_fallback(pkg, dev, monkeypatch):
+    """The DFT-GEMM path (HFG_MEL_DFT=1; the path for n_fft that are not a power of two)
+    still meets the float32 bounds."""
+    import importlib
+    monkeypatch.setenv("HFG_MEL_DFT", "1")
+    melmod = importlib.import_module("tts_sambert_hifigan_amd.mel")
+    from oracle import mel_torch as M
+    wav = _signals(5000)
+    got = melmod.MelSpectrogram(device=dev)(wav.to(dev)).cpu()
+    _check(got, M.log_mel(wav), fft=False)
 
 
 def test_extract_mel_contract(pkg, dev):

@@ -16,7 +16,8 @@ the same forward (oracle/hifigan_np64.py) by cond = max|ref_fp32 - ref_fp64|, an
 different fp32 summation order (MFMA vs oneDNN) legitimately lands anywhere within a
 few times that.
   fp32   : max|hip - ref| <= max(2e-6 * max(1, max|ref|), 4 * cond)
-  bf16x3 : max|hip - ref| <= max(2e-4 * max(1, max|ref|), 4 * cond)   (~16-bit-mantissa products)
+  bf16x3 : max|hip - ref| <= max(4e-5 * max(1, max|ref|), 4 * cond)   (~16-bit-mantissa products:
+           measured <= 2.5e-5 relative on every fixture, tests/tools/diag_precision.py)
 Also ResBlock.forward / MRF.forward called on their own (hfg_resblock_forward /
 hfg_mrf_forward) against the oracle.
 """
@@ -28,7 +29,7 @@ from conftest import golden_case_state, load_golden
 
 pytestmark = pytest.mark.gpu
 
-STAGE_RTOL = {"fp32": 2e-6, "bf16x3": 2e-4}
+STAGE_RTOL = {"fp32": 2e-6, "bf16x3": 4e-5}
 GOLDEN = ["g1_v1_b1_t32", "g2_v1_b2_t17", "g3_v2star_b2_t32", "g4_nonexact_b1_t20",
           "g5_v1_weightnorm_b1_t16", "g6_v1_loud2x_b1_t24", "g7_v1_b3_t1", "g8_v2star_b1_t3",
           "g9_v1_loud4x_b1_t24", "g10_v2star_loud4x_b1_t40"]
@@ -108,38 +109,58 @@ def test_stage_outputs_match_reference(pkg, golden_index, name, precision):
     assert torch.equal(plain, wav)
 
 
-@pytest.mark.parametrize("precision", ["fp32", "bf16x3"])
 @pytest.mark.parametrize("name", ["g9_v1_loud4x_b1_t24", "g10_v2star_loud4x_b1_t40"])
-def test_loud_x4_wav(pkg, golden_index, name, precision):
+def test_loud_x4_wav_fp32(pkg, golden_index, name):
     """x4 default-init weights: activations reach ~1e4-7e5 before
     conv_post, so tanh saturates and a sample near a zero crossing is as ill-conditioned
     as the stage values are large — the reference's own fp32 result differs from a
     float64 evaluation by up to 1.35e-3 there (golden_index.json np64_maxabs_diff).
-    The wav bar is therefore relative to that conditioning: every sample within
-    max(1e-4, 50 x |ref_fp32 - ref_fp64|_max) of the reference, and >= 99.5% of the
-    samples within 1e-4.  Per-stage parity (above) carries the precision evidence.
-
-    bf16x3 scale limit: its products carry ~16 mantissa bits, so at x4
-    scale a pre-tanh value of ~1e4 moves by ~0.1 and the few samples at the zero
-    crossings of a 99.8%-saturated tanh move with it.  For bf16x3 the x4 wav bar is
-    that documented limit: max error <= 0.15 and >= 99.5% of samples within 1e-4
-    (the 1e-4 guarantee holds up to the x2 fixture, g6)."""
+    Exact fp32 meets a bar relative to that conditioning: every sample within
+    max(1e-4, 50 x |ref_fp32 - ref_fp64|_max) of the reference, >= 99.5% within 1e-4.
+    (bf16x3 at this scale: test_bf16x3_scale_limits.)"""
     dev = _dev()
     case = golden_index["cases"][name]
     cfg, sd = golden_case_state(case)
     g = load_golden(name)
-    gen = _gen(pkg, cfg, sd, dev, precision)
+    gen = _gen(pkg, cfg, sd, dev, "fp32")
     with torch.no_grad():
         wav = gen(torch.from_numpy(g["mel"]).to(dev)).cpu().numpy()
     d = np.abs(wav - g["wav"])
     bound = max(1e-4, 50 * case["np64_maxabs_diff"])
-    if precision == "bf16x3":
-        bound = max(bound, 0.15)
     frac = float((d <= 1e-4).mean())
-    print(f"\n{name} [{precision}]: max|hip-ref| {d.max():.3e}, within 1e-4: {100 * frac:.3f}%, "
+    print(f"\n{name} [fp32]: max|hip-ref| {d.max():.3e}, within 1e-4: {100 * frac:.3f}%, "
           f"bound {bound:.2e}, saturated {(np.abs(g['wav']) > 0.999).mean():.3f}")
     assert d.max() <= bound
     assert frac >= 0.995
+
+
+def test_bf16x3_scale_limits(pkg, golden_index):
+    """The split-precision mode's documented scale limit (precision.BF16X3_SCALE_LIMITS,
+    carried by the bench line's dtype_note): on every golden fixture, by weight scale,
+    max|wav - reference| and the fraction of samples within 1e-4 meet the table — 1e-4
+    everywhere at x1 and x2, the stated bound at x4 (tanh zero crossings of a saturated
+    output; fp32 is the mode for such weights)."""
+    import importlib
+    P = importlib.import_module("tts_sambert_hifigan_amd.precision")
+    dev = _dev()
+    rows, seen = [], set()
+    for name in GOLDEN:
+        case = golden_index["cases"][name]
+        cfg, sd = golden_case_state(case)
+        g = load_golden(name)
+        gen = _gen(pkg, cfg, sd, dev, "bf16x3")
+        with torch.no_grad():
+            wav = gen(torch.from_numpy(g["mel"]).to(dev)).cpu().numpy()
+        d = np.abs(wav - g["wav"])
+        scale = float(case["weight_scale"])
+        lim = P.BF16X3_SCALE_LIMITS[scale]
+        frac = float((d <= 1e-4).mean())
+        rows.append(f"x{scale:g} {name}: max {d.max():.2e}, within 1e-4 {100 * frac:.2f}%")
+        assert d.max() <= lim["max_abs"], (name, d.max())
+        assert frac >= lim["within_1e-4"], (name, frac)
+        seen.add(scale)
+    print("\n" + "\n".join(rows))
+    assert seen == set(P.BF16X3_SCALE_LIMITS)
 
 
 @pytest.mark.parametrize("precision", ["fp32", "bf16x3"])

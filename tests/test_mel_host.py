@@ -157,3 +157,32 @@ def test_save_load_mel_roundtrip(tmp_path):
     m = torch.randn(80, 33)
     mel.save_mel(m, tmp_path / "sub" / "m.npy")
     assert torch.equal(mel.load_mel(tmp_path / "sub" / "m.npy"), m)
+
+
+def test_product_tables_bitwise_torch(pkg):
+    """The tables mel.MelSpectrogram hands the device (hfg_mel_set_tables) are bitwise the
+    float32 ones the reference's torchaudio builds: torch.hann_window (centred in n_fft)
+    and the melscale_fbanks restatement, for both scales and norms."""
+    import importlib
+    melmod = importlib.import_module("tts_sambert_hifigan_amd.mel")
+    for scale in ("slaney", "htk"):
+        for norm in ("slaney", None):
+            a = melmod.melscale_fbanks(513, 0.0, 8000.0, 80, 22050, norm, scale)
+            b = M.melscale_fbanks(513, 0.0, 8000.0, 80, 22050, norm, scale)
+            assert torch.equal(a, b), (scale, norm)
+    w = melmod.stft_window(1024, 800)
+    assert torch.equal(w[112:912], torch.hann_window(800)) and not w[:112].any()
+    assert not w[912:].any()
+
+
+def test_mel_set_tables_host_handle(pkg):
+    lib = pkg.load_library()
+    h = ctypes.c_void_p()
+    c = _cfg(pkg)
+    assert lib.hfg_mel_create(ctypes.byref(c), -1, ctypes.byref(h)) == 0
+    w = torch.hann_window(1024)
+    fb = M.melscale_fbanks(513, 0.0, 8000.0, 80, 22050, "slaney", "slaney").contiguous()
+    fp = ctypes.POINTER(ctypes.c_float)
+    assert lib.hfg_mel_set_tables(h, ctypes.cast(w.data_ptr(), fp), ctypes.cast(fb.data_ptr(), fp)) == 0
+    assert lib.hfg_mel_set_tables(h, None, None) == -22
+    lib.hfg_mel_destroy(h)

@@ -177,6 +177,7 @@ SIGNATURES = {
     "hfg_mel_create": (c_int, [POINTER(HfgMelConfig), c_int, POINTER(c_void_p)]),
     "hfg_mel_destroy": (None, [c_void_p]),
     "hfg_mel_filterbank": (c_int, [POINTER(HfgMelConfig), POINTER(c_float)]),
+    "hfg_mel_set_tables": (c_int, [c_void_p, POINTER(c_float), POINTER(c_float)]),
     "hfg_mel_frames": (c_int64, [c_void_p, c_int64]),
     "hfg_mel_workspace_bytes": (c_size_t, [c_void_p, c_int64, c_int64]),
     "hfg_mel_forward": (c_int, [c_void_p, c_void_p, c_int64, c_int64, c_void_p, c_void_p,
@@ -201,7 +202,12 @@ def load_library(path: str = LIB_PATH):
             "(python tts-sambert_hifigan_amd/build.py). There is no CPU fallback.")
     lib = ctypes.CDLL(path)
     for name, (res, args) in SIGNATURES.items():
-        fn = getattr(lib, name)
+        # an older build (a same-box A/B against a previous commit's library) may lack a
+        # newer entry point: it then fails when called; the build itself is checked to
+        # export every header symbol (tests/test_capi_host.py)
+        fn = getattr(lib, name, None)
+        if fn is None:
+            continue
         fn.restype = res
         fn.argtypes = args
     _lib = lib

@@ -170,8 +170,13 @@ conv1d_bf16x3(const ConvParams p) {
   // staging forms stays below that (byte offsets are unsigned 32-bit, as before)
   const __amdgpu_buffer_rsrc_t xrs =
       __builtin_amdgcn_make_buffer_rsrc((void*)xb, 0, -1, 0x00020000);
+  // whole 16-channel groups (every group of the V1 / V2* layers): the window mask and the
+  // pre-activation as max(v*s1, v*s2) like the AREG path (3 VALU per value instead of a
+  // per-element mask select + leaky_relu); partial groups keep the per-element mask
+  bool xfull = true;
   auto load_x = [&](int g) {
     const bool full = AREG || g * 16 + 16 <= p.C_in;  // block-uniform
+    xfull = full;
     xok = 0;
 #pragma unroll
     for (int q = 0; q < XQ; ++q) {
@@ -219,7 +224,7 @@ conv1d_bf16x3(const ConvParams p) {
 #pragma unroll
         for (int e = 0; e < 8; e += 2) {
           floatx2 a;
-          if constexpr (AREG) {
+          if (AREG || xfull) {
             a[0] = fmaxf(xv[q][e] * xs1[q], xv[q][e] * xs2[q]);
             a[1] = fmaxf(xv[q][e + 1] * xs1[q], xv[q][e + 1] * xs2[q]);
           } else {

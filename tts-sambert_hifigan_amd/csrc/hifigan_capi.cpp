@@ -1035,6 +1035,7 @@ int run_resblock(hfg_handle* h, Launcher& ln, const RbFused& rb, const float* x,
     p.mrf = last ? mrf : scratch;
     p.mrf_mode = last ? mrf_mode : 0;
     p.mrf_div = mrf_div;
+    p.mrf_rcp = hfg::fast_div_ok(mrf_div) ? 1.0f / mrf_div : 0.0f;
     p.dbg = h->dbg_flags;
     const double bytes =
         4.0 * B * Lt * C * ((last && (mrf_mode & 1)) ? 3 : 2) + 4.0 * (double)rb.w_len;

@@ -181,9 +181,15 @@ struct RbParams {
   float* mrf;            // MRF accumulator [B][C][L]
   int mrf_mode;          // bit0: add the existing value, bit1: divide by mrf_div
   float mrf_div;
+  float mrf_rcp;         // fp32(1 / mrf_div) when fast_div_ok(mrf_div) (exact fma quotient), else 0
   int dbg;               // ablations (HFG_DEBUG_FLAGS, wrong results when set): bit4 no MRF
                          // epilogue, bit5 no x loads, bit6 no operand writes
 };
+// divisors whose fma-refined reciprocal quotient equals the IEEE quotient for every fp32
+// input (div_exact, bf16x3_common.h; verified exhaustively, tests/tools/verify_fast_div.c)
+inline bool fast_div_ok(float d) {
+  return d == 1.f || d == 2.f || d == 3.f || d == 4.f || d == 5.f || d == 7.f || d == 8.f;
+}
 bool rb_supported(int C, int kt, int waves_n);
 size_t rb_lds_bytes(int C, int waves_n, int n_conv);
 hipError_t launch_resblock_bf16x3(int C, int waves_n, int kt, int np, const RbParams& p,

@@ -12,6 +12,7 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -57,7 +58,83 @@ struct hfg_mel_handle {
   float* tsin = nullptr;
   float* fb = nullptr;    // [n_bins][n_mels]
   std::vector<float> fb_host;
+  // FFT path (logmel_fft, n_fft a power of two): window [n_fft] fp32, twiddles [n_fft]
+  // complex double, per-band (first bin, end bin, offset) and the bands' nonzero weights
+  bool fft = false;
+  int fpw = 2;
+  float* win = nullptr;
+  void* tw = nullptr;
+  int* band = nullptr;
+  float* bw = nullptr;
 };
+
+namespace {
+
+// Build and upload every device table from a window [n_fft] and a filterbank
+// [n_bins][n_mels] (host, fp32): the DFT-GEMM path's windowed twiddles, the FFT path's
+// window, e^{-2 pi i t / N} (float64) and each band's nonzero bins.
+int upload_tables(hfg_mel_handle* h, const float* win, const float* fb) {
+  const hfg_mel_config* c = &h->cfg;
+  const int N = c->n_fft, n_mels = c->n_mels;
+  const double two_pi = 6.283185307179586476925286766559;
+  if (fb != h->fb_host.data()) h->fb_host.assign(fb, fb + (size_t)h->n_bins * n_mels);
+  std::vector<float> tc, ts;
+  if (!h->fft) {
+    tc.assign((size_t)N * h->bins_pad, 0.f);
+    ts.assign((size_t)N * h->bins_pad, 0.f);
+    for (int n = 0; n < N; ++n)
+      for (int k = 0; k < h->n_bins; ++k) {
+        const double ang = two_pi * (double)(((long long)k * n) % N) / N;
+        tc[(size_t)n * h->bins_pad + k] = (float)((double)win[n] * std::cos(ang));
+        ts[(size_t)n * h->bins_pad + k] = (float)(-(double)win[n] * std::sin(ang));
+      }
+  }
+  std::vector<double> tw_h(2 * (size_t)N);
+  for (int t = 0; t < N; ++t) {
+    tw_h[2 * t] = std::cos(two_pi * t / N);
+    tw_h[2 * t + 1] = -std::sin(two_pi * t / N);
+  }
+  std::vector<int> band_h(3 * (size_t)n_mels);
+  std::vector<float> bw_h;
+  for (int m = 0; m < n_mels; ++m) {
+    int lo = h->n_bins, hi = 0;
+    for (int k = 0; k < h->n_bins; ++k)
+      if (fb[(size_t)k * n_mels + m] != 0.f) {
+        lo = std::min(lo, k);
+        hi = k + 1;
+      }
+    if (hi <= lo) lo = hi = 0;
+    band_h[3 * m] = lo;
+    band_h[3 * m + 1] = hi;
+    band_h[3 * m + 2] = (int)bw_h.size();
+    for (int k = lo; k < hi; ++k) bw_h.push_back(fb[(size_t)k * n_mels + m]);
+  }
+  if (bw_h.empty()) bw_h.push_back(0.f);
+  if (h->device < 0) return HFG_OK;
+  int prev = -1;
+  (void)hipGetDevice(&prev);
+  if (hipSetDevice(h->device) != hipSuccess) return mfail(HFG_ENODEV, "hipSetDevice(%d)", h->device);
+  auto put = [&](void** dst, const void* src, size_t bytes) -> bool {
+    if (*dst) (void)hipFree(*dst);
+    *dst = nullptr;
+    if (hipMalloc(dst, bytes) != hipSuccess) return false;
+    return hipMemcpy(*dst, src, bytes, hipMemcpyHostToDevice) == hipSuccess;
+  };
+  bool ok = true;
+  if (!h->fft) {
+    ok = ok && put(reinterpret_cast<void**>(&h->tcos), tc.data(), tc.size() * 4);
+    ok = ok && put(reinterpret_cast<void**>(&h->tsin), ts.data(), ts.size() * 4);
+    ok = ok && put(reinterpret_cast<void**>(&h->fb), fb, h->fb_host.size() * 4);
+  }
+  ok = ok && put(reinterpret_cast<void**>(&h->win), win, (size_t)N * 4);
+  ok = ok && put(&h->tw, tw_h.data(), tw_h.size() * 8);
+  ok = ok && put(reinterpret_cast<void**>(&h->band), band_h.data(), band_h.size() * 4);
+  ok = ok && put(reinterpret_cast<void**>(&h->bw), bw_h.data(), bw_h.size() * 4);
+  if (prev >= 0) (void)hipSetDevice(prev);
+  return ok ? HFG_OK : mfail(HFG_ENOMEM, "mel tables: device allocation / copy failed");
+}
+
+}  // namespace
 
 extern "C" {
 
@@ -97,53 +174,39 @@ int hfg_mel_create(const hfg_mel_config* c, int device, hfg_mel_handle** out) {
     return mfail(HFG_EINVAL, "log_base: 10 (log10), 0 (ln) or 1 (custom base)");
   if (c->log_base == 1 && !(c->log_base_value > 0.f && c->log_base_value != 1.f))
     return mfail(HFG_EINVAL, "custom log base must be > 0 and != 1");
-  if ((size_t)(31 * c->hop_length + c->n_fft) * 4 * 33 / 32 > 64 * 1024)
-    return mfail(HFG_EINVAL, "n_fft / hop too large for the LDS frame tile");
+  // the DFT-GEMM path's LDS tiles (the fallback for n_fft that are not a power of two)
+  const bool dft_fits = (size_t)(31 * c->hop_length + c->n_fft) * 4 * 33 / 32 <= 64 * 1024 &&
+                        (size_t)16 * (c->n_fft / 2 + 1) * 4 <= 64 * 1024;
   auto* h = new (std::nothrow) hfg_mel_handle();
   if (!h) return mfail(HFG_ENOMEM, "host alloc");
   h->cfg = *c;
   h->device = device;
   h->n_bins = c->n_fft / 2 + 1;
   h->bins_pad = (h->n_bins + 31) / 32 * 32;
-  if ((size_t)16 * h->n_bins * 4 > 64 * 1024) {
-    delete h;
-    return mfail(HFG_EINVAL, "n_fft too large for the mel tile");
-  }
-  // windowed DFT tables: periodic Hann of win_length centred in n_fft (torch.stft)
+  // default tables: the periodic Hann window of win_length centred in n_fft (torch.stft)
+  // and torchaudio's filterbank, both evaluated in double and rounded to fp32 (the Python
+  // layer replaces them by the float32-evaluated torch tables, hfg_mel_set_tables)
   const int N = c->n_fft, W = c->win_length, left = (N - W) / 2;
-  std::vector<float> tc((size_t)N * h->bins_pad, 0.f), ts((size_t)N * h->bins_pad, 0.f);
   const double two_pi = 6.283185307179586476925286766559;
+  std::vector<float> win_h(N, 0.f);
   for (int n = 0; n < N; ++n) {
     const int wi = n - left;
-    const double w = (wi >= 0 && wi < W) ? 0.5 - 0.5 * std::cos(two_pi * wi / W) : 0.0;
-    for (int k = 0; k < h->n_bins; ++k) {
-      const double ang = two_pi * (double)(((long long)k * n) % N) / N;
-      tc[(size_t)n * h->bins_pad + k] = (float)(w * std::cos(ang));
-      ts[(size_t)n * h->bins_pad + k] = (float)(-w * std::sin(ang));
-    }
+    win_h[n] = (wi >= 0 && wi < W) ? (float)(0.5 - 0.5 * std::cos(two_pi * wi / W)) : 0.f;
   }
   h->fb_host.resize((size_t)h->n_bins * c->n_mels);
   hfg_mel_filterbank(c, h->fb_host.data());
-  if (device >= 0) {
-    int prev = -1;
-    (void)hipGetDevice(&prev);
-    if (hipSetDevice(device) != hipSuccess) {
-      delete h;
-      return mfail(HFG_ENODEV, "hipSetDevice(%d)", device);
-    }
-    const size_t tb = tc.size() * sizeof(float), fbb = h->fb_host.size() * sizeof(float);
-    if (hipMalloc(&h->tcos, tb) != hipSuccess || hipMalloc(&h->tsin, tb) != hipSuccess ||
-        hipMalloc(&h->fb, fbb) != hipSuccess) {
-      hfg_mel_destroy(h);
-      return mfail(HFG_ENOMEM, "hipMalloc(mel tables)");
-    }
-    if (hipMemcpy(h->tcos, tc.data(), tb, hipMemcpyHostToDevice) != hipSuccess ||
-        hipMemcpy(h->tsin, ts.data(), tb, hipMemcpyHostToDevice) != hipSuccess ||
-        hipMemcpy(h->fb, h->fb_host.data(), fbb, hipMemcpyHostToDevice) != hipSuccess) {
-      hfg_mel_destroy(h);
-      return mfail(HFG_EIO, "hipMemcpy(mel tables)");
-    }
-    if (prev >= 0) (void)hipSetDevice(prev);
+  h->fpw = N <= 1024 ? 2 : 1;
+  const char* md = getenv("HFG_MEL_DFT");  // 1: the DFT-GEMM path (A/B and fallback tests)
+  h->fft = (N & (N - 1)) == 0 && N >= 16 && !(md && atoi(md) != 0) &&
+           hfg::logmel_fft_lds_bytes(N, c->hop_length, h->fpw, c->n_mels) <= 160 * 1024;
+  if (!h->fft && !dft_fits) {
+    delete h;
+    return mfail(HFG_EINVAL, "n_fft / hop too large for the LDS frame tiles");
+  }
+  int rc = upload_tables(h, win_h.data(), h->fb_host.data());
+  if (rc) {
+    hfg_mel_destroy(h);
+    return rc;
   }
   *out = h;
   return HFG_OK;
@@ -154,7 +217,16 @@ void hfg_mel_destroy(hfg_mel_handle* h) {
   if (h->tcos) (void)hipFree(h->tcos);
   if (h->tsin) (void)hipFree(h->tsin);
   if (h->fb) (void)hipFree(h->fb);
+  if (h->win) (void)hipFree(h->win);
+  if (h->tw) (void)hipFree(h->tw);
+  if (h->band) (void)hipFree(h->band);
+  if (h->bw) (void)hipFree(h->bw);
   delete h;
+}
+
+int hfg_mel_set_tables(hfg_mel_handle* h, const float* window, const float* fb) {
+  if (!h || !window || !fb) return mfail(HFG_EINVAL, "NULL argument");
+  return upload_tables(h, window, fb);
 }
 
 int64_t hfg_mel_frames(const hfg_mel_handle* h, int64_t n_samples) {
@@ -183,15 +255,24 @@ int hfg_mel_forward(hfg_mel_handle* h, const float* wav, int64_t B, int64_t n_sa
   if (prev != h->device && hipSetDevice(h->device) != hipSuccess)
     return mfail(HFG_ENODEV, "hipSetDevice(%d)", h->device);
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const int log_mode = h->cfg.log_base == 10 ? 1 : (h->cfg.log_base == 0 ? 0 : 2);
+  // torch.log(torch.tensor(log_base)): a float32 log of the base
+  const float ln_base = std::log(h->cfg.log_base_value);
+  if (h->fft) {
+    hipError_t e = hfg::launch_logmel_fft(wav, B, n_samples, h->cfg.n_fft, h->cfg.hop_length,
+                                          n_frames, h->fpw, h->win, h->tw, h->band, h->bw,
+                                          h->cfg.n_mels, h->cfg.log_eps, log_mode, ln_base, mel, s);
+    if (prev >= 0 && prev != h->device) (void)hipSetDevice(prev);
+    if (e != hipSuccess) return mfail(HFG_EIO, "mel launch: %s", hipGetErrorString(e));
+    return HFG_OK;
+  }
   float* power = reinterpret_cast<float*>(workspace);
   hipError_t e = hfg::launch_stft_power(wav, B, n_samples, h->cfg.n_fft, h->cfg.hop_length,
                                         h->n_bins, n_frames, h->tcos, h->tsin, h->bins_pad, power,
                                         s);
   if (e == hipSuccess)
     e = hfg::launch_mel_log(power, B, n_frames, h->n_bins, h->fb, h->cfg.n_mels, h->cfg.log_eps,
-                            h->cfg.log_base == 10 ? 1 : (h->cfg.log_base == 0 ? 0 : 2),
-                            // torch.log(torch.tensor(log_base)): a float32 log of the base
-                            std::log(h->cfg.log_base_value), mel, s);
+                            log_mode, ln_base, mel, s);
   if (prev >= 0 && prev != h->device) (void)hipSetDevice(prev);
   if (e != hipSuccess) return mfail(HFG_EIO, "mel launch: %s", hipGetErrorString(e));
   return HFG_OK;

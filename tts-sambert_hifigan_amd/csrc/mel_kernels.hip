@@ -14,6 +14,7 @@
 
 #include <cstdint>
 
+#include "kernels.h"
 #include "mel_kernels.h"
 
 namespace hfg {
@@ -99,6 +100,205 @@ mel_log(const float* __restrict__ power, int n_frames, int n_bins, const float* 
     mel[((int64_t)b * n_mels + m) * n_frames + f0 + f] =
         log_mode == 1 ? log10f(v) : (log_mode == 0 ? logf(v) : logf(v) / ln_base);
   }
+}
+
+// ---------------------------------------------------------------------------------------
+// logmel_fft: the whole log-mel of a tile of frames in one launch, FFT-based.
+//
+// Per frame (one wave): z[n] = w[2n] x[2n] + i w[2n+1] x[2n+1] (the window product in fp32,
+// as torch.stft forms it), an N/2-point complex FFT in float64 by mixed-radix Stockham passes
+// (radix 8, then 4 or 2) ping-ponging between two LDS buffers, the real-FFT split
+// X[k] = (Z[k] + Z*[N/2-k]) / 2 - i e^{-2 pi i k / N} (Z[k] - Z*[N/2-k]) / 2 for
+// k = 0..N/2, |X|^2, the slaney / htk mel projection over each band's nonzero bins, + eps,
+// log.  float64 arithmetic makes the spectrum exact to ~1e-15 of the frame energy, so quiet
+// bins (silence beside loud frames) keep their precision; the O(N log N) FFT replaces the
+// O(N^2) DFT GEMM (stft_power_mfma, kept for n_fft that are not a power of two).
+// Block: 4 waves x fpw frames; the block's reflect-padded sample span is staged once in
+// LDS (fp32) and the [n_mels][frames] tile leaves through LDS as frame-contiguous rows.
+struct cd {
+  double x, y;
+};
+__device__ __forceinline__ cd cmul(cd a, cd b) {
+  return {a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x};
+}
+__device__ __forceinline__ cd cadd(cd a, cd b) { return {a.x + b.x, a.y + b.y}; }
+__device__ __forceinline__ cd csub(cd a, cd b) { return {a.x - b.x, a.y - b.y}; }
+__device__ __forceinline__ cd cmul_mi(cd a) { return {a.y, -a.x}; }  // (-i) a
+
+// in-register DFT of R points: out[q] = sum_r v[r] e^{-2 pi i r q / R}
+template <int R>
+__device__ __forceinline__ void dft_r(cd (&v)[R]);
+template <>
+__device__ __forceinline__ void dft_r<2>(cd (&v)[2]) {
+  const cd a = cadd(v[0], v[1]), b = csub(v[0], v[1]);
+  v[0] = a;
+  v[1] = b;
+}
+template <>
+__device__ __forceinline__ void dft_r<4>(cd (&v)[4]) {
+  const cd t0 = cadd(v[0], v[2]), t1 = csub(v[0], v[2]);
+  const cd t2 = cadd(v[1], v[3]), t3 = cmul_mi(csub(v[1], v[3]));
+  v[0] = cadd(t0, t2);
+  v[2] = csub(t0, t2);
+  v[1] = cadd(t1, t3);
+  v[3] = csub(t1, t3);
+}
+template <>
+__device__ __forceinline__ void dft_r<8>(cd (&v)[8]) {
+  cd e[4] = {v[0], v[2], v[4], v[6]}, o[4] = {v[1], v[3], v[5], v[7]};
+  dft_r<4>(e);
+  dft_r<4>(o);
+  constexpr double s = 0.70710678118654752440;
+  o[1] = {s * (o[1].x + o[1].y), s * (o[1].y - o[1].x)};   // e^{-i pi/4}
+  o[2] = cmul_mi(o[2]);                                      // e^{-i pi/2}
+  o[3] = {s * (o[3].y - o[3].x), -s * (o[3].x + o[3].y)};  // e^{-3i pi/4}
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    v[q] = cadd(e[q], o[q]);
+    v[q + 4] = csub(e[q], o[q]);
+  }
+}
+
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// one Stockham pass of radix R over an N2-point sequence: sub-transforms of Ns -> Ns * R
+// points (twiddle e^{-2 pi i r k / (Ns R)} = tw[2 r k N2 / (Ns R) mod N], tw[t] =
+// e^{-2 pi i t / N}, N = 2 N2)
+template <int R>
+__device__ __forceinline__ void stockham_pass(const cd* __restrict__ src, cd* __restrict__ dst,
+                                              int N2, int Ns, const cd* __restrict__ tw,
+                                              int lane) {
+  const int nb = N2 / R;
+  const int tstep = 2 * (N2 / (Ns * R));
+  for (int j = lane; j < nb; j += 64) {
+    const int k = j & (Ns - 1);
+    cd v[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) v[r] = src[j + r * nb];
+    if (Ns > 1) {
+#pragma unroll
+      for (int r = 1; r < R; ++r) v[r] = cmul(v[r], tw[(r * k * tstep) & (2 * N2 - 1)]);
+    }
+    dft_r<R>(v);
+    const int base = (j - k) * R + k;
+#pragma unroll
+    for (int q = 0; q < R; ++q) dst[base + q * Ns] = v[q];
+  }
+}
+
+__global__ void __launch_bounds__(256)
+logmel_fft(const float* __restrict__ wav, int64_t n_samp, int n_fft, int hop, int n_frames,
+           int fpw, const float* __restrict__ window, const cd* __restrict__ tw,
+           const int* __restrict__ band, const float* __restrict__ bw, int n_mels, float eps,
+           int log_mode, float ln_base, float* __restrict__ mel) {
+  extern __shared__ __attribute__((aligned(16))) char lds_m[];
+  const int N2 = n_fft / 2;
+  const int fpb = 4 * fpw;
+  const int span = (fpb - 1) * hop + n_fft;
+  cd* const bufs = reinterpret_cast<cd*>(lds_m);                        // [4 waves][2][N2]
+  float* const sig = reinterpret_cast<float*>(lds_m + sizeof(cd) * 8 * N2);  // [span]
+  float* const mel_s = sig + ((span + 3) & ~3);                         // [n_mels][fpb]
+  const int b = blockIdx.y;
+  const int f0 = blockIdx.x * fpb;
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const float* x = wav + (int64_t)b * n_samp;
+  // reflect-padded samples [f0 hop - N/2, f0 hop - N/2 + span)  (torch reflect: x[-i] = x[i],
+  // x[L-1+i] = x[L-1-i]; the host checks L > N/2)
+  for (int i = threadIdx.x; i < span; i += 256) {
+    int64_t g = (int64_t)f0 * hop - N2 + i;
+    if (g < 0) g = -g;
+    if (g >= n_samp) g = 2 * (n_samp - 1) - g;
+    sig[i] = (g >= 0 && g < n_samp) ? x[g] : 0.f;
+  }
+  __syncthreads();
+  cd* A = bufs + (size_t)wave * 2 * N2;
+  cd* Bf = A + N2;
+  for (int fi = 0; fi < fpw; ++fi) {
+    const int fl = wave * fpw + fi;  // frame within the block
+    if (f0 + fl >= n_frames) break;  // wave-uniform
+    const float* fr = sig + fl * hop;
+    for (int n = lane; n < N2; n += 64) {
+      const float x0 = fr[2 * n] * window[2 * n], x1 = fr[2 * n + 1] * window[2 * n + 1];
+      A[n] = {(double)x0, (double)x1};
+    }
+    wave_sync();
+    cd* src = A;
+    cd* dst = Bf;
+    int Ns = 1, rem = __builtin_ctz(N2);
+    while (rem > 0) {
+      if (rem >= 3) {
+        stockham_pass<8>(src, dst, N2, Ns, tw, lane);
+        Ns *= 8;
+        rem -= 3;
+      } else if (rem == 2) {
+        stockham_pass<4>(src, dst, N2, Ns, tw, lane);
+        Ns *= 4;
+        rem -= 2;
+      } else {
+        stockham_pass<2>(src, dst, N2, Ns, tw, lane);
+        Ns *= 2;
+        rem -= 1;
+      }
+      wave_sync();
+      cd* t = src;
+      src = dst;
+      dst = t;
+    }
+    // real-FFT split and power, k = 0..N2, into the free buffer as doubles
+    double* P = reinterpret_cast<double*>(dst);
+    for (int k = lane; k <= N2; k += 64) {
+      const cd zk = src[k & (N2 - 1)];
+      const cd zm = src[(N2 - k) & (N2 - 1)];
+      const cd zc = {zm.x, -zm.y};
+      const cd s_ = cadd(zk, zc), d_ = csub(zk, zc);
+      const cd wd = cmul(tw[k], d_);                 // e^{-2 pi i k/N} (Z[k] - Z*[N2-k])
+      const double re = 0.5 * (s_.x + wd.y), im = 0.5 * (s_.y - wd.x);  // (s - i wd) / 2
+      P[k] = re * re + im * im;
+    }
+    wave_sync();
+    for (int m = lane; m < n_mels; m += 64) {
+      const int lo = band[3 * m], hi = band[3 * m + 1], off = band[3 * m + 2];
+      double acc = 0.0;
+      for (int k = lo; k < hi; ++k) acc += (double)bw[off + k - lo] * P[k];
+      const double v = acc + (double)eps;
+      const double lv = log_mode == 1 ? log10(v) : (log_mode == 0 ? log(v) : log(v) / (double)ln_base);
+      mel_s[m * fpb + fl] = (float)lv;
+    }
+    wave_sync();
+  }
+  __syncthreads();
+  const int nf = min(fpb, n_frames - f0);
+  for (int i = threadIdx.x; i < n_mels * fpb; i += 256) {
+    const int m = i / fpb, fl = i - m * fpb;
+    if (fl < nf) mel[((int64_t)b * n_mels + m) * n_frames + f0 + fl] = mel_s[m * fpb + fl];
+  }
+}
+
+size_t logmel_fft_lds_bytes(int n_fft, int hop, int fpw, int n_mels) {
+  const int fpb = 4 * fpw;
+  const size_t span = (size_t)(fpb - 1) * hop + n_fft;
+  return sizeof(cd) * 8 * (size_t)(n_fft / 2) + sizeof(float) * ((span + 3) & ~(size_t)3) +
+         sizeof(float) * (size_t)n_mels * fpb;
+}
+
+hipError_t launch_logmel_fft(const float* wav, int64_t B, int64_t n_samp, int n_fft, int hop,
+                             int n_frames, int fpw, const float* window, const void* tw,
+                             const int* band, const float* bw, int n_mels, float eps,
+                             int log_mode, float ln_base, float* mel, hipStream_t stream) {
+  if (n_fft < 16 || (n_fft & (n_fft - 1)) || fpw < 1) return hipErrorInvalidValue;
+  const size_t lds = logmel_fft_lds_bytes(n_fft, hop, fpw, n_mels);
+  if (lds > 160 * 1024) return hipErrorInvalidValue;
+  if (hipError_t err = ensure_max_lds(reinterpret_cast<const void*>(logmel_fft))) return err;
+  dim3 grid((n_frames + 4 * fpw - 1) / (4 * fpw), (unsigned)B);
+  logmel_fft<<<grid, dim3(256), lds, stream>>>(wav, n_samp, n_fft, hop, n_frames, fpw, window,
+                                               reinterpret_cast<const cd*>(tw), band, bw, n_mels,
+                                               eps, log_mode, ln_base, mel);
+  return hipGetLastError();
 }
 
 hipError_t launch_stft_power(const float* wav, int64_t B, int64_t N, int n_fft, int hop,

@@ -92,13 +92,8 @@ resblock_bf16x3(const RbParams p) {
   for (int i = tid; i < n_conv * C; i += NT) bias_s[i] = p.bias[i];
 
   bool vk[WN];
-  bool wave_valid = true;  // every column of this wave inside [0, len)
 #pragma unroll
-  for (int k = 0; k < WN; ++k) {
-    vk[k] = (unsigned)(ws + cbase + 32 * k + col) < (unsigned)len_b;
-    wave_valid = wave_valid && (unsigned)(ws + cbase + 32 * k) < (unsigned)len_b &&
-                 (unsigned)(ws + cbase + 32 * k + 31) < (unsigned)len_b;
-  }
+  for (int k = 0; k < WN; ++k) vk[k] = (unsigned)(ws + cbase + 32 * k + col) < (unsigned)len_b;
 
   // ---- A stream (buffer loads: SGPR descriptor + scalar step offset, no address VALU) ----
   const __amdgpu_buffer_rsrc_t wrs =
@@ -115,28 +110,45 @@ resblock_bf16x3(const RbParams p) {
   load_a(0, Q0);
   load_a(1, Q0 + 1);
 
+  // ---- x and the MRF accumulator of utterance b through buffer descriptors ----
+  // Element (row, column) sits at soffset = (row0 + row part of accumulator element r) * L * 4
+  // (wave-uniform: SALU) + voffset = (4 * half * L + column) * 4 (one VGPR per column tile):
+  // no per-element address VALU and no branches.  An item is at most 2^30 floats, so every
+  // offset fits 32 bits; the range is never relied on (masked lanes read offset 0).
+  const unsigned Lb = (unsigned)p.L * 4u;
+  auto srow = [&](int r) { return (unsigned)(row0 + (r & 3) + 8 * (r >> 2)) * Lb; };
+  const unsigned lrow = 4u * (unsigned)half * (unsigned)p.L;
+  const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(p.x + (int64_t)b * p.bs), 0, (int)0xFFFFFFFFu, 0x00020000);
+
   // ---- residual stream x: window -> registers (zero outside [0, len)) ----
   floatx16 xcur[WN];
   {
-    const float* __restrict__ xb = p.x + (int64_t)b * p.bs;
 #pragma unroll
     for (int k = 0; k < WN; ++k) {
-      const int ta = ws + cbase + 32 * k + col;
+      const unsigned vo = vk[k] ? (lrow + (unsigned)(ws + cbase + 32 * k + col)) * 4u : 0u;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const unsigned off = vk[k] ? (unsigned)((row0 + rrow(r)) * p.L + ta) : 0u;
-        xcur[k][r] = (dbg & 32) ? 0.f : xb[off];
-      }
+      for (int r = 0; r < 16; ++r)
+        xcur[k][r] = __builtin_bit_cast(
+            float, __builtin_amdgcn_raw_buffer_load_b32(xrs, (int)vo, (int)srow(r), 0));
     }
+    // ablation bit 5 zeroes x after the loads (a select on a uniform flag inside the load
+    // expression made the compiler branch per element)
+    const bool xz = dbg & 32;
 #pragma unroll
     for (int k = 0; k < WN; ++k)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) xcur[k][r] = vk[k] ? xcur[k][r] : 0.f;
+      for (int r = 0; r < 16; ++r) xcur[k][r] = (vk[k] && !xz) ? xcur[k][r] : 0.f;
   }
 
   // lane's byte address of window column (cbase + col) in its half-group's hi plane
   const int vb = half * HPS + (cbase + col + MARG) * 16;
 
+  // leaky_relu and the zero padding as one max(v * f1, v * f2) per value: (1, 0.1) inside
+  // [0, len) = bitwise max(v, 0.1 v), (0, 0) outside = 0 (3 VALU ops, no select; both
+  // operands are products, so no canonicalising max of the raw value is needed)
+  // (the factors are formed per write from vk: kept live across the kernel they cost the
+  // C = 128 instance 16 VGPRs and spills)
   // B operand of the next conv: lrelu(v), zero outside [0, len), split hi/lo -> LDS.
   // The 8 accumulator rows a lane holds per 16-channel group are exactly the 8 slots
   // (one 16-B row of its half-group) it reads as a B fragment.
@@ -144,20 +156,18 @@ resblock_bf16x3(const RbParams p) {
     if (dbg & 64) return;
 #pragma unroll
     for (int k = 0; k < WN; ++k) {
+      const floatx2 f1k = vk[k] ? 1.0f : 0.0f, f2k = vk[k] ? kLReluSlope : 0.0f;
 #pragma unroll
       for (int gg = 0; gg < 2; ++gg) {
         bf16x8 h, l;
 #pragma unroll
         for (int e = 0; e < 8; e += 2) {
-          floatx2 a;
-          a[0] = v[k][gg * 8 + e];
-          a[1] = v[k][gg * 8 + e + 1];
-          a[0] = lrelu3(a[0]);
-          a[1] = lrelu3(a[1]);
-          if (!wave_valid) {
-            a[0] = vk[k] ? a[0] : 0.f;
-            a[1] = vk[k] ? a[1] : 0.f;
-          }
+          floatx2 vv, a;
+          vv[0] = v[k][gg * 8 + e];
+          vv[1] = v[k][gg * 8 + e + 1];
+          const floatx2 p1 = vv * f1k, p2 = vv * f2k;  // v_pk_mul_f32
+          a[0] = fmaxf(p1[0], p2[0]);
+          a[1] = fmaxf(p1[1], p2[1]);
           const bf16x2 hh = __builtin_convertvector(a, bf16x2);
           const floatx2 hf = __builtin_convertvector(hh, floatx2);
           const bf16x2 ll = __builtin_convertvector(a - hf, bf16x2);
@@ -251,45 +261,59 @@ resblock_bf16x3(const RbParams p) {
     if (xcur[0][0] == 1.2345e-30f) p.mrf[0] = xcur[WN - 1][15];
     return;
   }
-  float* __restrict__ mb = p.mrf + (int64_t)b * p.bs;
+  const __amdgpu_buffer_rsrc_t mrs = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(p.mrf + (int64_t)b * p.bs), 0, (int)0xFFFFFFFFu, 0x00020000);
   const bool add = p.mrf_mode & 1;
   const bool div = p.mrf_mode & 2;
-  // every column tile's MRF loads are issued before any store (the stores may alias later
-  // tiles' loads as far as the compiler knows, so a per-tile loop paid one HBM round trip
-  // per tile); the accumulators are dead here, so the 16 x WN loaded values fit
-  unsigned rowoff[16];
-#pragma unroll
-  for (int r = 0; r < 16; ++r) rowoff[r] = (unsigned)((row0 + rrow(r)) * p.L);
   bool ok[WN];
-  unsigned ta[WN];
+  unsigned vo[WN];
 #pragma unroll
   for (int k = 0; k < WN; ++k) {
     const int c = cbase + 32 * k + col;
     ok[k] = vk[k] && c >= p.halo && c < p.halo + p.W;
-    ta[k] = ok[k] ? (unsigned)(ws + c) : 0u;
+    vo[k] = ok[k] ? (lrow + (unsigned)(ws + c)) * 4u : 0u;
   }
-  // offsets formed at each access (one add) instead of 16 x WN live registers
-  auto off = [&](int k, int r) { return ok[k] ? rowoff[r] + ta[k] : 0u; };
+  // every MRF load is issued before any use (one wait for all 16 x WN), then the adds /
+  // divisions for every tile; the empty asm keeps the compiler from sinking a tile's loads
+  // into its store branch (which serialised one HBM round trip per element)
   if (add) {
     float mv[WN][16];
 #pragma unroll
     for (int k = 0; k < WN; ++k)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) mv[k][r] = mb[off(k, r)];
+      for (int r = 0; r < 16; ++r)
+        mv[k][r] = __builtin_bit_cast(
+            float, __builtin_amdgcn_raw_buffer_load_b32(mrs, (int)vo[k], (int)srow(r), 0));
 #pragma unroll
     for (int k = 0; k < WN; ++k)
 #pragma unroll
       for (int r = 0; r < 16; ++r) xcur[k][r] = mv[k][r] + xcur[k][r];
   }
+  if (div && p.mrf_rcp != 0.f) {
 #pragma unroll
-  for (int k = 0; k < WN; ++k) {
-    if (div) {
+    for (int k = 0; k < WN; ++k)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) xcur[k][r] = div_fast(xcur[k][r], p.mrf_div, p.mrf_rcp);
+  } else if (div) {
+#pragma unroll
+    for (int k = 0; k < WN; ++k)
 #pragma unroll
       for (int r = 0; r < 16; ++r) xcur[k][r] = xcur[k][r] / p.mrf_div;
-    }
+  }
+#pragma unroll
+  for (int k = 0; k < WN; ++k)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) asm volatile("" ::"v"(xcur[k][r]));
+#pragma unroll
+  for (int k = 0; k < WN; ++k) {
     if (ok[k]) {
 #pragma unroll
-      for (int r = 0; r < 16; ++r) mb[off(k, r)] = xcur[k][r];
+      for (int r = 0; r < 16; ++r) {
+        // through a scalar: __builtin_bit_cast of an ext_vector element lvalue compiled to
+        // element 0 of the vector (every row stored the same value)
+        const float v = xcur[k][r];
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), mrs, (int)vo[k], (int)srow(r), 0);
+      }
     }
   }
 }

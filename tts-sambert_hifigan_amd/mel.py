@@ -10,8 +10,8 @@ Mirrors ``data/audio_processing.py``:
 * :func:`extract_mel_from_file` (:142-164), :func:`save_mel` / :func:`load_mel`
   (:167-200), :func:`load_config` (:16-28).
 
-The arithmetic runs in the HIP kernels of ``libhifigan_hip.so``: the windowed DFT on
-the fp32 matrix cores + mel projection + log (:class:`MelSpectrogram`, the batched
+The arithmetic runs in the HIP kernels of ``libhifigan_hip.so``: one launch of an
+FFT with a float64 spectrum + mel projection + log (:class:`MelSpectrogram`, the batched
 ``[B, N] → [B, n_mels, N // hop + 1]`` form that feeds ``HiFiGANGenerator``), and the
 polyphase sinc resampler (:class:`Resample`, torchaudio ``Resample`` defaults).
 There is no CPU fallback: a CPU waveform raises.
@@ -44,6 +44,58 @@ def _log_base_code(log_base):
     return 1, float(log_base)
 
 
+# torchaudio.functional.melscale_fbanks / _hz_to_mel / _mel_to_hz, evaluated with the same
+# float32 torch ops (the reference's MelSpectrogram builds its filterbank this way,
+# audio_processing.py:99-110), so the device tables are bitwise the reference's
+def _hz_to_mel(freq: float, mel_scale: str) -> float:
+    import math
+    if mel_scale == "htk":
+        return 2595.0 * math.log10(1.0 + freq / 700.0)
+    f_sp, min_log_hz = 200.0 / 3, 1000.0
+    mels = freq / f_sp
+    if freq >= min_log_hz:
+        mels = min_log_hz / f_sp + math.log(freq / min_log_hz) / (math.log(6.4) / 27.0)
+    return mels
+
+
+def _mel_to_hz(mels: torch.Tensor, mel_scale: str) -> torch.Tensor:
+    import math
+    if mel_scale == "htk":
+        return 700.0 * (10.0 ** (mels / 2595.0) - 1.0)
+    f_sp, min_log_hz = 200.0 / 3, 1000.0
+    freqs = f_sp * mels
+    min_log_mel = min_log_hz / f_sp
+    logstep = math.log(6.4) / 27.0
+    log_t = mels >= min_log_mel
+    freqs[log_t] = min_log_hz * torch.exp(logstep * (mels[log_t] - min_log_mel))
+    return freqs
+
+
+def melscale_fbanks(n_freqs: int, f_min: float, f_max: float, n_mels: int, sample_rate: int,
+                    norm: Optional[str], mel_scale: str) -> torch.Tensor:
+    """[n_freqs, n_mels] float32 triangular filterbank (torchaudio's algorithm)."""
+    all_freqs = torch.linspace(0, sample_rate // 2, n_freqs)
+    m_pts = torch.linspace(_hz_to_mel(f_min, mel_scale), _hz_to_mel(f_max, mel_scale), n_mels + 2)
+    f_pts = _mel_to_hz(m_pts, mel_scale)
+    f_diff = f_pts[1:] - f_pts[:-1]
+    slopes = f_pts.unsqueeze(0) - all_freqs.unsqueeze(1)
+    down = (-1.0 * slopes[:, :-2]) / f_diff[:-1]
+    up = slopes[:, 2:] / f_diff[1:]
+    fb = torch.max(torch.zeros(1), torch.min(down, up))
+    if norm == "slaney":
+        fb *= (2.0 / (f_pts[2:n_mels + 2] - f_pts[:n_mels])).unsqueeze(0)
+    return fb
+
+
+def stft_window(n_fft: int, win_length: int) -> torch.Tensor:
+    """torch.stft's effective window: torch.hann_window(win_length) (periodic, float32)
+    zero-padded to n_fft, centred."""
+    w = torch.zeros(n_fft)
+    left = (n_fft - win_length) // 2
+    w[left:left + win_length] = torch.hann_window(win_length)
+    return w
+
+
 class MelSpectrogram:
     """torchaudio.transforms.MelSpectrogram(power=2) + log on the HIP device."""
 
@@ -71,6 +123,15 @@ class MelSpectrogram:
         _check_mel(self.lib, self.lib.hfg_mel_create(ctypes.byref(c), self.device.index or 0,
                                                      ctypes.byref(h)))
         self.ptr = h
+        # the reference's float32 window and filterbank (bitwise torch.stft / torchaudio)
+        self._window = stft_window(n_fft, win_length).contiguous()
+        self._fb = melscale_fbanks(n_fft // 2 + 1, float(f_min), float(f_max), n_mels,
+                                   sample_rate, norm, mel_scale).contiguous()
+        fp = ctypes.POINTER(ctypes.c_float)
+        if not hasattr(self.lib, "hfg_mel_set_tables"):  # an older library (A/B runs)
+            return
+        _check_mel(self.lib, self.lib.hfg_mel_set_tables(
+            self.ptr, ctypes.cast(self._window.data_ptr(), fp), ctypes.cast(self._fb.data_ptr(), fp)))
 
     def __del__(self):
         try:
@@ -81,10 +142,12 @@ class MelSpectrogram:
             pass
 
     def filterbank(self) -> torch.Tensor:
-        fb = torch.zeros(self.cfg.n_fft // 2 + 1, self.n_mels)
-        self.lib.hfg_mel_filterbank(ctypes.byref(self.cfg),
-                                    ctypes.cast(fb.data_ptr(), ctypes.POINTER(ctypes.c_float)))
-        return fb
+        """The [n_fft/2+1, n_mels] filterbank the device uses (torchaudio's, float32)."""
+        return self._fb.clone()
+
+    def window(self) -> torch.Tensor:
+        """The [n_fft] window the device uses (torch.hann_window(win_length), centred)."""
+        return self._window.clone()
 
     def frames(self, n_samples: int) -> int:
         return n_samples // self.hop + 1
