@@ -409,7 +409,7 @@ def extra_configs(pkg, S, dev, precision, steps=5):
         t = timed(lambda: ext(audio), 20)
         out["mel_8x262144"] = {"ms": t * 1e3, "frames_per_s": 8 * (262144 // 256 + 1) / t,
                                "audio_samples_per_s": 8 * 262144 / t,
-                               "note": "hfg_mel_forward: windowed DFT on the fp32 MFMA + mel + log10"}
+                               "note": "hfg_mel_forward: framing + real FFT (float64 Stockham in LDS) + mel + log in one launch"}
         rs = melmod.Resample(16000, 22050, device=dev)
         a16 = torch.randn(8, 16000, generator=g).clamp(-1, 1).to(dev)
         for _ in range(2):

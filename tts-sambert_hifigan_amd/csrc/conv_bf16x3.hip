@@ -221,6 +221,15 @@ conv1d_bf16x3(const ConvParams p) {
       const int i = tid + q * NT;
       if (AREG || i < 2 * XW) {
         bf16x8 h, l;
+        if (UPS && (p.dbg & 256)) {
+          // ablation (upsamplers, timing only): the raw fp32 halves, no pre-activation or split
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const unsigned u = __float_as_uint(xv[q][e]);
+            h[e] = __builtin_bit_cast(__bf16, (unsigned short)(u >> 16));
+            l[e] = __builtin_bit_cast(__bf16, (unsigned short)(u & 0xffffu));
+          }
+        } else
 #pragma unroll
         for (int e = 0; e < 8; e += 2) {
           floatx2 a;
