@@ -124,3 +124,18 @@ def test_package_imports_by_underscore_name():
                          capture_output=True, text=True, timeout=300)
     assert out.returncode == 0, out.stderr
     assert out.stdout.split() == ["tts_sambert_hifigan_amd.hifigan", "tts-sambert_hifigan_amd"]
+
+
+def test_default_precision_from_environment(pkg, monkeypatch):
+    """Constructor default: exact fp32, or HFG_PRECISION (a reference code base switches its
+    Generator to the split-precision path without code changes); submodules follow."""
+    monkeypatch.delenv("HFG_PRECISION", raising=False)
+    assert pkg.HiFiGANGenerator(**C.V2STAR.kwargs()).precision == "fp32"
+    monkeypatch.setenv("HFG_PRECISION", "bf16x3")
+    gen = pkg.HiFiGANGenerator(**C.V2STAR.kwargs())
+    assert gen.precision == "bf16x3"
+    assert {m.precision for m in gen.mrfs} == {"bf16x3"}
+    assert pkg.HiFiGANGenerator(**C.V2STAR.kwargs(), precision="fp32").precision == "fp32"
+    monkeypatch.setenv("HFG_PRECISION", "fp16")
+    with pytest.raises(ValueError):
+        pkg.HiFiGANGenerator(**C.V2STAR.kwargs())

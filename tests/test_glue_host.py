@@ -74,7 +74,9 @@ def test_multi_stream_batched_equals_one_shot_and_is_bounded(pkg):
     for s in range(S):
         assert torch.equal(torch.cat(outs[s]), ref[s]), s
     assert max(gen.calls) > 1  # streams really shared forwards
-    assert max(sv.capacity(s) for s in range(S)) <= chunk + 2 * 3 + 9 + 9
+    # fixed per-stream buffers: live columns + slack for the gather and a few chunks
+    w = chunk + 2 * 3
+    assert max(sv.capacity(s) for s in range(S)) <= 2 * (w + 9) + w + (w + 9)
 
 
 def test_single_stream_push_flush_constant_state(pkg, capsys):
@@ -90,6 +92,9 @@ def test_single_stream_push_flush_constant_state(pkg, capsys):
     pieces.append(sv.flush())
     assert torch.equal(torch.cat(pieces), ref)
     assert len(caps) == 1  # one allocation for the whole stream
+    # trimming moves an offset; the live columns are copied back to the front only
+    # every few chunks
+    assert 0 < sv.compactions <= sv.chunks_run // 2
     lines = [l for l in capsys.readouterr().out.splitlines() if l.startswith("[StreamingVocoder]")]
     assert len(lines) == sv.chunks_run == -(-2000 // 16)
     assert "mel (1, 5, " in lines[1] and "-> wav (64,)" in lines[1]

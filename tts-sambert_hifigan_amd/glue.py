@@ -54,18 +54,20 @@ class StreamingVocoder:
     which an output sample does not depend on the input: no overlap-add or crossfade is
     needed, the seams are exact).  Needs an exact-upsampling config (out = T x hop).
 
-    Bounded state: a stream keeps only the frames ``[emitted - context, received)`` in
-    a per-stream buffer of fixed capacity (``chunk + 2 context`` + the largest push so
-    far), so memory and per-push cost do not grow with the stream's length.
+    Bounded state: a stream keeps only the frames ``[emitted - context, received)``.  Each
+    stream owns one fixed buffer whose live columns start at a moving offset: a step only
+    advances the offset past frames no later chunk reads (no copy), and the live columns
+    move back to the front only when a feed would run past the end (amortised over several
+    chunks), so memory and per-step cost do not grow with the stream's length.
 
     Several streams (``n_streams``) share each forward: :meth:`feed` appends frames
     without computing, :meth:`step` vocodes the next ready chunk of EVERY stream as one
     ragged batch (per-item lengths, ``hfg_forward_ex``; each item equals its window
-    run alone, so batching changes no sample), :meth:`finish` marks a stream's end so
-    its tail is emitted by the following steps.  :meth:`push` / :meth:`flush` are the
-    one-stream convenience (feed, then step until nothing is ready).  With
-    ``debug_shapes`` (default: the generator's, i.e. ``DEBUG_SHAPES=1``) every chunk
-    prints its shapes (Requirement 18.4).
+    run alone, so batching changes no sample; the batch is gathered from the stream
+    buffers in one copy), :meth:`finish` marks a stream's end so its tail is emitted by
+    the following steps.  :meth:`push` / :meth:`flush` are the one-stream convenience
+    (feed, then step until nothing is ready).  With ``debug_shapes`` (default: the
+    generator's, i.e. ``DEBUG_SHAPES=1``) every chunk prints its shapes (Requirement 18.4).
     """
 
     def __init__(self, gen, chunk_frames: int = 64, context: Optional[int] = None,
@@ -81,12 +83,17 @@ class StreamingVocoder:
         self.n_streams = int(n_streams)
         self.debug_shapes = (getattr(gen, "debug_shapes", False) if debug_shapes is None
                              else bool(debug_shapes))
+        # widest window a step reads; a gathered window may run past a stream's live
+        # columns by up to this much (read, never used: the forward masks by length)
+        self._wmax = self.chunk + 2 * self.ctx
         self._buf: List[Optional[torch.Tensor]] = [None] * self.n_streams  # [n_mels, cap]
-        self._start = [0] * self.n_streams     # absolute frame index of _buf[s][:, 0]
-        self._fill = [0] * self.n_streams      # valid columns of _buf[s]
+        self._pos = [0] * self.n_streams       # buffer column of frame _start
+        self._start = [0] * self.n_streams     # absolute frame index of the first live column
+        self._fill = [0] * self.n_streams      # live columns
         self._done = [False] * self.n_streams
         self._emitted = [0] * self.n_streams   # frames whose audio was returned
         self.chunks_run = 0
+        self.compactions = 0
 
     # -- state -------------------------------------------------------------------------
     @property
@@ -113,16 +120,25 @@ class StreamingVocoder:
         t = frames.shape[1]
         if t == 0:
             return
-        buf, fill = self._buf[stream], self._fill[stream]
-        need = fill + t
-        if buf is None or need > buf.shape[1] or buf.device != frames.device:
-            cap = max(need, self.chunk + 2 * self.ctx + t)
-            nb = torch.empty(frames.shape[0], cap, dtype=torch.float32, device=frames.device)
-            if buf is not None and fill:
-                nb[:, :fill].copy_(buf[:, :fill])
-            self._buf[stream] = buf = nb
-        buf[:, fill:need].copy_(frames)
-        self._fill[stream] = need
+        buf, pos, fill = self._buf[stream], self._pos[stream], self._fill[stream]
+        # invariant after a feed: pos + fill + wmax <= cap (a step's gather stays in bounds)
+        if buf is None or buf.device != frames.device or pos + fill + t + self._wmax > buf.shape[1]:
+            if (buf is not None and buf.device == frames.device
+                    and fill + t + self._wmax <= buf.shape[1]):
+                if fill:  # live columns back to the front; overlapping ranges: clone first
+                    src = buf[:, pos:pos + fill]
+                    buf[:, :fill].copy_(src.clone() if fill > pos else src)
+                self.compactions += 1
+            else:
+                # room for a few chunks of slack: a compaction every ~2 chunks at most
+                cap = 2 * (self.chunk + 2 * self.ctx + t) + self._wmax + fill
+                nb = torch.zeros(frames.shape[0], cap, dtype=torch.float32, device=frames.device)
+                if buf is not None and fill:
+                    nb[:, :fill].copy_(buf[:, pos:pos + fill])
+                self._buf[stream] = buf = nb
+            self._pos[stream] = pos = 0
+        buf[:, pos + fill:pos + fill + t].copy_(frames)
+        self._fill[stream] = fill + t
 
     def finish(self, stream: int = 0) -> None:
         """No more frames for `stream`: its remaining audio is emitted by later steps."""
@@ -142,17 +158,14 @@ class StreamingVocoder:
         return a, b, max(0, a - self.ctx), min(T, b + self.ctx)
 
     def _trim(self, s: int) -> None:
-        """Drop frames no future chunk reads: keep [emitted - ctx, received)."""
+        """Drop frames no future chunk reads (keep [emitted - ctx, received)): the live
+        range's offset moves, nothing is copied."""
         keep_from = max(self._start[s], self._emitted[s] - self.ctx)
         drop = keep_from - self._start[s]
         if drop > 0:
-            buf, fill = self._buf[s], self._fill[s]
-            rest = fill - drop
-            if rest > 0:
-                # regions overlap when rest > drop: clone the source first
-                buf[:, :rest].copy_(buf[:, drop:fill].clone() if rest > drop else buf[:, drop:fill])
+            self._pos[s] += drop
             self._start[s] = keep_from
-            self._fill[s] = rest
+            self._fill[s] -= drop
 
     def step(self, streams: Optional[Sequence[int]] = None) -> Dict[int, torch.Tensor]:
         """One batched forward over every stream (of `streams`, default all) with a ready
@@ -163,12 +176,13 @@ class StreamingVocoder:
             return {}
         lens = [hi - lo for _, (a, b, lo, hi) in ready]
         W = max(lens)
-        dev = self._buf[ready[0][0]].device
-        n_mels = self._buf[ready[0][0]].shape[0]
-        mel = torch.zeros(len(ready), n_mels, W, dtype=torch.float32, device=dev)
-        for i, (s, (a, b, lo, hi)) in enumerate(ready):
-            off = lo - self._start[s]
-            mel[i, :, :hi - lo].copy_(self._buf[s][:, off:off + hi - lo])
+        # one gather (a batched copy of the strided windows); columns past an item's length
+        # are whatever the buffer holds there: the forward reads a ragged item only below
+        # its length
+        views = [self._buf[s][:, self._pos[s] + lo - self._start[s]:
+                              self._pos[s] + lo - self._start[s] + W]
+                 for s, (a, b, lo, hi) in ready]
+        mel = torch.stack(views)
         with torch.no_grad():
             wav = self.gen(mel, lengths=None if min(lens) == W else lens)
         out = {}

@@ -26,7 +26,7 @@ from __future__ import annotations
 
 import os
 import weakref
-from typing import Dict, List, Tuple
+from typing import Dict, List, Optional, Tuple
 
 import torch
 import torch.nn as nn
@@ -46,6 +46,28 @@ def _on_param_registered(module, name, param):
 
 
 nn.modules.module.register_module_parameter_registration_hook(_on_param_registered)
+
+
+def _lengths_on(lengths, device) -> torch.Tensor:
+    """Per-item lengths as a contiguous int32 tensor on `device`.  A host list goes through
+    pinned memory with a non-blocking copy: a pageable host-to-device copy would make the
+    host wait for all work already queued on the stream (every ragged forward a sync)."""
+    if isinstance(lengths, torch.Tensor) and lengths.device == device:
+        return lengths.to(torch.int32).contiguous()
+    host = torch.as_tensor(lengths).to(torch.int32).contiguous()
+    if host.device.type == "cpu":
+        host = host.pin_memory()
+    return host.to(device, non_blocking=True)
+
+
+def default_precision() -> str:
+    """The precision a module gets when its constructor is not given one: "fp32" (exact),
+    or ``HFG_PRECISION`` from the environment ("fp32", "bf16x3", "bf16w"), so a reference
+    code base can switch its Generator to the split-precision path without code changes."""
+    p = os.environ.get("HFG_PRECISION", "fp32")
+    if p not in ("fp32", "bf16x3", "bf16w"):
+        raise ValueError(f"HFG_PRECISION={p!r}: expected fp32, bf16x3 or bf16w")
+    return p
 
 
 def get_padding(kernel_size: int, dilation: int = 1) -> int:
@@ -71,7 +93,8 @@ class _HipWeights(nn.Module):
 
     verify_weights = False
 
-    def _hip_setup(self, precision: str):
+    def _hip_setup(self, precision: Optional[str]):
+        precision = default_precision() if precision is None else precision
         self._hfg_handles: Dict[int, _lib.Handle] = {}
         self._hfg_fingerprint: Dict[int, tuple] = {}
         self._hfg_checksum: Dict[int, torch.Tensor] = {}
@@ -195,7 +218,7 @@ class ResBlock(_HipWeights):
     it runs ``hfg_resblock_forward`` on an MRF handle of this one block."""
 
     def __init__(self, channels: int, kernel_size: int = 3, dilation: Tuple[int, ...] = (1, 3, 5),
-                 *, precision: str = "fp32"):
+                 *, precision: Optional[str] = None):
         super().__init__()
         self.channels = channels
         self.kernel_size = kernel_size
@@ -231,8 +254,9 @@ class MRF(_HipWeights):
 
     def __init__(self, channels: int, resblock_kernel_sizes: List[int] = [3, 7, 11],
                  resblock_dilation_sizes: List[List[int]] = [[1, 3, 5], [1, 3, 5], [1, 3, 5]],
-                 *, precision: str = "fp32"):
+                 *, precision: Optional[str] = None):
         super().__init__()
+        precision = default_precision() if precision is None else precision
         self.channels = channels
         self.resblock_kernel_sizes = list(resblock_kernel_sizes)
         self.resblock_dilation_sizes = [list(d) for d in resblock_dilation_sizes]
@@ -271,9 +295,10 @@ class HiFiGANGenerator(_HipWeights):
         resblock_dilation_sizes: List[List[int]] = [[1, 3, 5], [1, 3, 5], [1, 3, 5]],
         debug_shapes: bool = False,
         *,
-        precision: str = "fp32",
+        precision: Optional[str] = None,
     ):
         super().__init__()
+        precision = default_precision() if precision is None else precision
         self.n_mels = n_mels
         self.num_kernels = len(resblock_kernel_sizes)
         self.num_upsamples = len(upsample_rates)
@@ -296,7 +321,7 @@ class HiFiGANGenerator(_HipWeights):
         self._hfg_args = (n_mels, upsample_rates, upsample_kernel_sizes, upsample_initial_channel,
                           resblock_kernel_sizes, resblock_dilation_sizes)
         self._hip_setup(precision)
-        self.set_precision(precision)
+        self.set_precision(self.precision)
 
     def set_precision(self, precision: str):
         """"fp32" (exact fp32 MFMA, default), "bf16x3" (fp32 operands split into
@@ -383,10 +408,9 @@ class HiFiGANGenerator(_HipWeights):
             else:
                 lens_t = None
                 if lengths is not None:
-                    lens_t = torch.as_tensor(lengths).to(device=mel.device, dtype=torch.int32)
+                    lens_t = _lengths_on(lengths, mel.device)
                     if lens_t.shape != (B,):
                         raise RuntimeError(f"lengths must have shape [{B}]")
-                    lens_t = lens_t.contiguous()
                 h.forward_ex(mel_c.data_ptr(), B, T, wav.data_ptr(), out_len, ws.data_ptr(),
                              ws_bytes, stream, mel_layout=mel_layout,
                              lengths_ptr=lens_t.data_ptr() if lens_t is not None else 0)
@@ -489,7 +513,7 @@ class HiFiGAN(nn.Module):
                  resblock_dilation_sizes: List[List[int]] = [[1, 3, 5], [1, 3, 5], [1, 3, 5]],
                  msd_use_spectral_norm: bool = False, mpd_periods: List[int] = [2, 3, 5, 7, 11],
                  mpd_use_spectral_norm: bool = False, debug_shapes: bool = False, *,
-                 precision: str = "fp32"):
+                 precision: Optional[str] = None):
         super().__init__()
         self.debug_shapes = debug_shapes or os.getenv("DEBUG_SHAPES", "0") == "1"
         self.generator = HiFiGANGenerator(
