@@ -138,14 +138,26 @@ def test_c5_sambert_batch32_ragged(pkg, dev, c5, precision):
     print(f"\nC5 [{precision}] 32 utterances, frames {min(lens)}-{max(lens)}: max err {worst:.2e}")
 
 
-@pytest.mark.parametrize("precision", ["bf16x3", "fp32"])
-def test_v2star_thin_stages_ragged_and_vs_layer_kernels(pkg, dev, precision):
-    """The V2* C = 16 / 8 stages run as one mrf_thin launch per MRF (csrc/mrf_thin.hip):
+@pytest.mark.parametrize("precision,thin_mfma", [("bf16x3", None), ("bf16x3", "1"),
+                                                  ("fp32", None)])
+def test_v2star_thin_stages_ragged_and_vs_layer_kernels(pkg, dev, precision, thin_mfma):
+    """The V2* C = 16 / 8 stages run as one thin launch per MRF (csrc/mrf_thin.hip, and
+    csrc/mrf_thin_mfma.hip for bf16x3: C = 16 by default, C = 8 too with HFG_THIN_MFMA=1):
     a ragged batch equals each utterance run alone (bitwise, zero past its length), and
     the thin path agrees with the layer-per-launch kernels (HFG_THIN=0) and the oracle."""
     from oracle import config as C, hifigan_torch as H
     cfg = C.V2STAR
     sd = C.make_state_dict(cfg, seed=21)
+    # read when the handle is created (first forward): set for the whole test
+    if thin_mfma is not None:
+        os.environ["HFG_THIN_MFMA"] = thin_mfma
+    try:
+        _thin_case(pkg, dev, precision, cfg, sd, H)
+    finally:
+        os.environ.pop("HFG_THIN_MFMA", None)
+
+
+def _thin_case(pkg, dev, precision, cfg, sd, H):
     gen = _gen(pkg, cfg, sd, dev, precision)
     g = torch.Generator().manual_seed(7)
     lens = [37, 64, 5, 50]
@@ -163,7 +175,15 @@ def test_v2star_thin_stages_ragged_and_vs_layer_kernels(pkg, dev, precision):
         wav_l = _run(gen_l, mel.to(dev))
     finally:
         del os.environ["HFG_THIN"]
+    h = gen.hip_handle(dev)
+    h.profile_reset()
+    h.set_profiling(True)
     wav_t = _run(gen, mel.to(dev))
+    h.set_profiling(False)
+    names = " ".join(h.profile_summary())
+    if precision == "bf16x3":
+        assert "mrf_thin_mfma<16" in names
+        assert ("mrf_thin_mfma<8" in names) == (os.environ.get("HFG_THIN_MFMA") == "1"), names
     err = (wav_t - wav_l).abs().max().item()
     print(f"\nV2* thin vs layer kernels [{precision}]: {err:.2e}")
     assert err < 2e-5

@@ -231,6 +231,16 @@ hipError_t launch_mrf_thin(int C, const ThinParams& p, int batch, hipStream_t st
 // the same MRF on the bf16 matrix cores in split precision (v_mfma_f32_16x16x32_bf16):
 // 4 waves x kThinMfmaTiles 16-column tiles (a 512-column window), C in {8, 16}
 constexpr int kThinMfmaTiles = 8;
+// operand buffers of mrf_thin_mfma: 2 = one barrier per conv (conv1 / conv2 alternate),
+// 1 = rewritten in place (two barriers per conv; round 2)
+#ifndef HFG_THIN_BUFS
+#define HFG_THIN_BUFS 2
+#endif
+constexpr int kThinMfmaBufs = HFG_THIN_BUFS;
+// C = 8 row-half sum: v_permlane32_swap (1) or a ds_bpermute shuffle (0)
+#ifndef HFG_THIN_SWAP
+#define HFG_THIN_SWAP 1
+#endif
 constexpr int kThinMfmaMaxSteps = 4;  // k-steps per conv (k <= 7 for C = 16, <= 15 for C = 8)
 int thin_mfma_window(int C);  // 0: unsupported C
 size_t thin_mfma_lds_bytes(int C);

@@ -77,12 +77,13 @@ mrf_thin_mfma(const ThinParams p) {
 #pragma unroll
   for (int t = 0; t < NCT; ++t) vk[t] = (unsigned)(ws + cbase + 16 * t) < (unsigned)len_b;
 
-  // zero the margin rows of both planes once (operand writes cover the window only)
+  // zero the margin rows of every plane once (operand writes cover the window only)
   for (int i = tid; i < 2 * MARG * RB / 4; i += NW * 64) {
     const int row = i / (RB / 4), w4 = i - row * (RB / 4);
     const int r = row < MARG ? row : NWIN + row;
-    *reinterpret_cast<float*>(lds + r * RB + w4 * 4) = 0.f;
-    *reinterpret_cast<float*>(lds + PS + r * RB + w4 * 4) = 0.f;
+#pragma unroll
+    for (int pl = 0; pl < 2 * kThinMfmaBufs; ++pl)
+      *reinterpret_cast<float*>(lds + pl * PS + r * RB + w4 * 4) = 0.f;
   }
 
   // channel of accumulator element i (C = 8: the row halves are combined, rows 8-15
@@ -101,7 +102,7 @@ mrf_thin_mfma(const ThinParams p) {
   const int a_lane = lane * 16;
 
   // operand <- lrelu(v), zero outside [0, len), hi/lo split (lanes of rows 8-15 idle for C=8)
-  auto write_operand = [&](const floatx4 (&v)[NCT]) {
+  auto write_operand = [&](const floatx4 (&v)[NCT], char* buf) {
     if (C == 8 && q >= 2) return;
 #pragma unroll
     for (int t = 0; t < NCT; ++t) {
@@ -120,8 +121,8 @@ mrf_thin_mfma(const ThinParams p) {
         l[i + 1] = ll[1];
       }
       const int off = opnd_off(cbase + 16 * t + MARG, chan(0));
-      *reinterpret_cast<bf16x4*>(lds + off) = h;
-      *reinterpret_cast<bf16x4*>(lds + PS + off) = l;
+      *reinterpret_cast<bf16x4*>(buf + off) = h;
+      *reinterpret_cast<bf16x4*>(buf + PS + off) = l;
     }
   };
 
@@ -146,8 +147,8 @@ mrf_thin_mfma(const ThinParams p) {
   };
   // acc = bias + W_cv * operand, with (a0, a1) = conv cv's A fragments; the next conv's
   // are loaded into (n0, n1)
-  auto run_conv = [&](int cv, const bf16x8 (&a0)[MS], const bf16x8 (&a1)[MS], bf16x8 (&n0)[MS],
-                      bf16x8 (&n1)[MS]) {
+  auto run_conv = [&](int cv, const char* buf, const bf16x8 (&a0)[MS], const bf16x8 (&a1)[MS],
+                      bf16x8 (&n0)[MS], bf16x8 (&n1)[MS]) {
     load_a(n0, n1, cv + 1);
     const int kt = p.kt[cv], d = p.dil[cv];
     const int steps = (kt + TPS - 1) / TPS;
@@ -162,8 +163,8 @@ mrf_thin_mfma(const ThinParams p) {
     bf16x8 bh[2], bl[2];
     auto load_b = [&](int slot, int s, int t) {
       const int off = opnd_off(row_q + s * TPS * d + 16 * t, ch_q);
-      bh[slot] = *reinterpret_cast<const bf16x8*>(lds + off);
-      bl[slot] = *reinterpret_cast<const bf16x8*>(lds + PS + off);
+      bh[slot] = *reinterpret_cast<const bf16x8*>(buf + off);
+      bl[slot] = *reinterpret_cast<const bf16x8*>(buf + PS + off);
     };
     load_b(0, 0, 0);
 #pragma unroll
@@ -193,7 +194,17 @@ mrf_thin_mfma(const ThinParams p) {
       if constexpr (C == 8) {
         // rows 0-7 (lanes 0-31) + rows 8-15 (lanes 32-63): both halves get the same sum
 #pragma unroll
-        for (int i = 0; i < 4; ++i) acc[t][i] = acc[t][i] + __shfl_xor(acc[t][i], 32, 64);
+        for (int i = 0; i < 4; ++i) {
+#if HFG_THIN_SWAP
+          // v_permlane32_swap: (lo, hi) = (lanes 0-31 keep own | get lower, lanes 0-31 get
+          // upper | keep own), so lo + hi = lower + upper in both halves (the shuffle's sum)
+          const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(acc[t][i]),
+                                                          __float_as_uint(acc[t][i]), false, false);
+          acc[t][i] = __uint_as_float(sw[0]) + __uint_as_float(sw[1]);
+#else
+          acc[t][i] = acc[t][i] + __shfl_xor(acc[t][i], 32, 64);
+#endif
+        }
       }
 #pragma unroll
       for (int i = 0; i < 4; ++i) acc[t][i] = acc[t][i] + bv[i];
@@ -217,14 +228,19 @@ mrf_thin_mfma(const ThinParams p) {
       }
     const int cv0 = p.rb_conv0[r], cv1 = p.rb_conv0[r + 1];
     for (int cv = cv0; cv < cv1; cv += 2) {
-      __syncthreads();  // the previous conv's operand reads are done
-      write_operand(xr);
+      // two operand buffers (kThinMfmaBufs = 2): conv1 reads buffer 0, conv2 buffer 1, so a
+      // buffer is rewritten only after the barrier that follows every read of it (one
+      // barrier per conv); one buffer: rewritten in place between two barriers
+      char* const b0 = lds;
+      char* const b1 = lds + (kThinMfmaBufs - 1) * 2 * PS;
+      if (kThinMfmaBufs == 1) __syncthreads();  // the previous conv's operand reads are done
+      write_operand(xr, b0);
       __syncthreads();
-      run_conv(cv, sa0, sa1, sb0, sb1);
+      run_conv(cv, b0, sa0, sa1, sb0, sb1);
+      if (kThinMfmaBufs == 1) __syncthreads();
+      write_operand(acc, b1);
       __syncthreads();
-      write_operand(acc);
-      __syncthreads();
-      run_conv(cv + 1, sb0, sb1, sa0, sa1);
+      run_conv(cv + 1, b1, sb0, sb1, sa0, sa1);
 #pragma unroll
       for (int t = 0; t < NCT; ++t) xr[t] = acc[t] + xr[t];  // xt + x, :85
     }
@@ -275,7 +291,7 @@ EntryThinMfma* find_thin_mfma(int C, int np = 3) {
 int thin_mfma_window(int C) { return find_thin_mfma(C) ? 4 * kThinMfmaTiles * 16 : 0; }
 
 size_t thin_mfma_lds_bytes(int C) {
-  return (size_t)2 * (4 * kThinMfmaTiles * 16 + 2 * kThinMarg) * 2 * C;
+  return (size_t)kThinMfmaBufs * 2 * (4 * kThinMfmaTiles * 16 + 2 * kThinMarg) * 2 * C;
 }
 
 hipError_t launch_mrf_thin_mfma(int C, int np, const ThinParams& p, int batch,
