@@ -205,3 +205,38 @@ def test_bf16x3_layer_kernels_run_to_run_bitwise(pkg, big_tile, fused, monkeypat
     for o in outs[1:]:
         for a, b in zip(outs[0], o):
             assert np.array_equal(a, b), np.abs(a - b).max()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("precision", ["bf16x3", "bf16w"])
+@pytest.mark.parametrize("preset,B,T,lens", [("v1", 3, 64, [64, 41, 3]),
+                                             ("v2star", 2, 64, [64, 17]),
+                                             ("nonexact", 2, 64, [64, 29])])
+def test_ups_frames_kernel_bitwise(pkg, preset, B, T, lens, precision, monkeypatch):
+    """The output-frame upsampler kernel (csrc/ups_bf16x3.hip: k = 2u stages, both sample
+    classes of a frame per wave) gives the polyphase conv1d_bf16x3 upsampler's result bit
+    for bit: the same MFMA sequence per output element, the same split of lrelu(x), the
+    same zero padding.  HFG_UPS_FRAMES=2 forces it onto every eligible stage (rates 8 and 2
+    in V1 / V2*, 4 and 2 in the non-exact preset; rate 5 stays polyphase), 0 keeps the
+    polyphase kernel; ragged and full batches."""
+    from oracle import config as C, prng
+    dev = _dev()
+    cfg = C.PRESETS[preset]
+    sd = C.make_state_dict(cfg, seed=31)
+    mel = torch.as_tensor(prng.mel_input(31 + T, (B, cfg.n_mels, T))).to(dev)
+    ln = torch.tensor(lens, dtype=torch.int32, device=dev)
+    outs, names = {}, {}
+    for mode in ("0", "2"):
+        monkeypatch.setenv("HFG_UPS_FRAMES", mode)  # read when the handle is created
+        gen = _gen(pkg, cfg, sd, dev, precision=precision)
+        h = gen.hip_handle(dev)
+        h.profile_reset()
+        h.set_profiling(True)
+        with torch.no_grad():
+            outs[mode] = (gen(mel).cpu().numpy(), gen(mel, lengths=ln).cpu().numpy())
+        torch.cuda.synchronize()
+        h.set_profiling(False)
+        names[mode] = " ".join(h.profile_summary())
+    assert "ups_bf16x3<" in names["2"] and "ups_bf16x3<" not in names["0"], names
+    for a, b in zip(outs["0"], outs["2"]):
+        assert np.array_equal(a, b), np.abs(a - b).max()

@@ -81,6 +81,10 @@ struct Layer {
   // bf16x3 layers: a second packing for the small-grid tile (kBf16x3SmallTile), -1: none
   int tile_s = -1, m_tiles_s = 0, n_chunks_s = 0;
   size_t ws_off = 0, bs_off = 0;
+  // bf16x3 upsamplers with k = 2u: the output-frame kernel (ups_bf16x3.hip) on its own
+  // packing, -1: none
+  int ups_cfg = -1, m_tiles_f = 0;
+  size_t wf_off = 0, bf_off = 0;
 };
 
 // bf16x3 and bf16w both run the split-operand bf16 MFMA kernels
@@ -167,6 +171,9 @@ struct hfg_handle {
                              // (HFG_RB_WN32: 4 or 8)
   bool mfma16 = true;        // 16x16x32-shape ResBlock kernel for C = 32 (HFG_MFMA16=0: off)
   int ups_swizzle = 1;       // XCD swizzle of the upsampler blocks (HFG_UPS_SWIZZLE=0: off)
+  int ups_frames = 1;        // k = 2u upsamplers on the output-frame kernel: 1 when its grid
+                             // fills the chip, 2 always, 0 never (HFG_UPS_FRAMES; the
+                             // polyphase conv1d_bf16x3 path gives the bitwise same result)
   int np = 3;                // MFMA products per multiply-add: 3 (bf16x3), 2 (bf16w: lo(w) = 0)
   int areg = 1;              // tile-3 layer convs on tile 5 (A in registers; HFG_AREG=0: off)
   int epi_lds = 1;           // LDS-staged float4 epilogue of the bf16x3 layer convs (HFG_EPI_LDS=0: off)
@@ -372,6 +379,24 @@ int build_layers(hfg_handle* h) {
                ~(size_t)63;
         L.bs_off = off;
         off += ((size_t)L.m_tiles_s * ts.MT() + 63) & ~(size_t)63;
+      }
+      // k = 2u upsamplers (padding u/2): the output-frame kernel's own packing
+      const int rows_f = L.kind == L_UPS ? L.C_out * L.s / 2 : 0;
+      if (L.kind == L_UPS && h->ups_frames && L.k == 2 * L.s && hfg::ups_rate_ok(L.s) &&
+          L.p == L.s / 2 && L.C_in % 16 == 0) {
+        const int cfg = rows_f % hfg::kUpsCfgs[0].MT() == 0   ? 0
+                        : rows_f % hfg::kUpsCfgs[1].MT() == 0 ? 1
+                                                               : -1;
+        if (cfg >= 0) {
+          const hfg::UpsCfg& tf = hfg::kUpsCfgs[cfg];
+          L.ups_cfg = cfg;
+          L.m_tiles_f = rows_f / tf.MT();
+          L.wf_off = off;
+          // bf16: m-tiles x groups x (class, tap, plane) x rows x 16 ch
+          off += ((size_t)L.m_tiles_f * (L.C_in / 16) * 8 * tf.MT() * 16 / 2 + 63) & ~(size_t)63;
+          L.bf_off = off;
+          off += ((size_t)L.C_out + 63) & ~(size_t)63;
+        }
       }
       continue;
     }
@@ -708,6 +733,40 @@ void pack_resblock(hfg_handle* h, const RbFused& rb) {
   }
 }
 
+// A slabs of ups_bf16x3 (ups_bf16x3.hip), in bf16 elements:
+//   idx = (((((((mt*n_g + g)*2 + c)*2 + tp)*2 + plane)*WAVES_M + wave_m)*WM + wm)*64 + lane)*8 + e
+//   class row rr = mt*MT + wave_m*32*WM + wm*32 + (lane & 31) -> co = rr / h, s' = rr % h
+//   (h = u/2), ci = g*16 + 8*(lane >> 5) + e; kernel index (nn.ConvTranspose1d weight
+//   [C_in][C_out][k]): class L (c = 0) tap 0 (x[m-1]) s'+h+u, tap 1 (x[m]) s'+h;
+//   class R (c = 1) tap 0 (x[m]) s'+u, tap 1 (x[m+1]) s'.  Bias [C_out].
+void pack_ups_frames(hfg_handle* h, const Layer& L) {
+  const hfg::UpsCfg& t = hfg::kUpsCfgs[L.ups_cfg];
+  const float* w = h->params[L.mod + ".weight"].data.data();
+  const float* bias = h->params[L.mod + ".bias"].data.data();
+  uint16_t* dst = reinterpret_cast<uint16_t*>(h->packed_host.data() + L.wf_off);
+  const int u = L.s, hh = u / 2, k = L.k, cout = L.C_out, n_g = L.C_in / 16;
+  size_t idx = 0;
+  for (int mt = 0; mt < L.m_tiles_f; ++mt)
+    for (int g = 0; g < n_g; ++g)
+      for (int c = 0; c < 2; ++c)
+        for (int tp = 0; tp < 2; ++tp)
+          for (int plane = 0; plane < 2; ++plane)
+            for (int wave_m = 0; wave_m < t.WAVES_M; ++wave_m)
+              for (int wm = 0; wm < t.WM; ++wm)
+                for (int lane = 0; lane < 64; ++lane)
+                  for (int e = 0; e < 8; ++e) {
+                    const int rr = mt * t.MT() + wave_m * 32 * t.WM + wm * 32 + (lane & 31);
+                    const int co = rr / hh, sp = rr % hh;
+                    const int ci = g * 16 + 8 * (lane >> 5) + e;
+                    const int j = c == 0 ? (tp == 0 ? sp + hh + u : sp + hh) : (tp == 0 ? sp + u : sp);
+                    const float v = w[((size_t)ci * cout + co) * k + j];
+                    const uint16_t hi = f2bf(v);
+                    dst[idx++] = plane == 0 ? hi : f2bf(v - bf2f(hi));
+                  }
+  float* bdst = h->packed_host.data() + L.bf_off;
+  for (int co = 0; co < cout; ++co) bdst[co] = bias[co];
+}
+
 void pack_layer(hfg_handle* h, const Layer& L) {
   const Param& W = h->params[L.mod + ".weight"];
   const Param& Bp = h->params[L.mod + ".bias"];
@@ -750,6 +809,7 @@ void pack_layer(hfg_handle* h, const Layer& L) {
         for (size_t m = 0; m < Lp.b_len; ++m) bd[m] = m < (size_t)L.M ? Bp.data[m / s] : 0.f;
       }
     }
+    if (L.ups_cfg >= 0) pack_ups_frames(h, L);
     return;
   }
   if (L.kind == L_CONV) {
@@ -1053,6 +1113,41 @@ int run_resblock(hfg_handle* h, Launcher& ln, const RbFused& rb, const float* x,
 
 int run_ups(hfg_handle* h, Launcher& ln, const Layer& L, const float* x, int64_t B, int64_t Lin,
             int64_t Lout, float* y, const int32_t* len_in, const int32_t* len_out) {
+  const double flop = 2.0 * L.C_in * L.C_out * L.k * (double)Lin * B;
+  const double bytes = 4.0 * B * (L.C_in * Lin + L.C_out * Lout) + 4.0 * L.C_in * L.C_out * L.k;
+  if (L.ups_cfg >= 0 && h->ups_frames && Lin % 4 == 0 && Lout == Lin * L.s) {
+    // output-frame kernel, unless its grid would leave most CUs idle (then the polyphase
+    // kernel's small-grid tile): bitwise the same result either way
+    const hfg::UpsCfg& t = hfg::kUpsCfgs[L.ups_cfg];
+    const int n_tiles = (int)((Lin + t.NTILE() - 1) / t.NTILE());
+    if (h->ups_frames == 2 ||
+        (int64_t)L.m_tiles_f * n_tiles * B * ln.conc >= hfg::kSmallGridBlocks) {
+      hfg::UpsParams q{};
+      q.x = x;
+      q.x_bs = (int64_t)L.C_in * Lin;
+      q.C_in = L.C_in;
+      q.L = (int)Lin;
+      q.T = (int)Lin;
+      q.len_in = len_in;
+      q.w = reinterpret_cast<const __bf16*>(h->packed_dev + L.wf_off);
+      q.bias = h->packed_dev + L.bf_off;
+      q.y = y;
+      q.y_bs = (int64_t)L.C_out * Lout;
+      q.C_out = L.C_out;
+      q.L_out = (int)Lout;
+      q.u = L.s;
+      q.m_tiles = L.m_tiles_f;
+      q.n_tiles = n_tiles;
+      q.batch = (int)B;
+      const char* name = nullptr;
+      ln.begin(flop, bytes);
+      hipError_t e = hfg::launch_ups_bf16x3(L.ups_cfg, h->np, q, ln.stream, &name);
+      ln.end(name);
+      if (e != hipSuccess)
+        return fail(HFG_EIO, "launch %s: %s", L.mod.c_str(), hipGetErrorString(e));
+      return HFG_OK;
+    }
+  }
   ConvParams p{};
   p.x = x;
   p.x_bs = (int64_t)L.C_in * Lin;
@@ -1083,8 +1178,6 @@ int run_ups(hfg_handle* h, Launcher& ln, const Layer& L, const float* x, int64_t
   const int ntile = L.prec == 1 ? hfg::kBf16x3Tiles[L.tile].NTILE() : kTiles[L.tile].NTILE();
   int n_tiles = (p.N + ntile - 1) / ntile, m_tiles = L.m_tiles;
   const int tile = pick_tile(h, L, p, p.N, B, ln.conc, n_tiles, m_tiles);
-  const double flop = 2.0 * L.C_in * L.C_out * L.k * (double)Lin * B;
-  const double bytes = 4.0 * B * (L.C_in * Lin + L.C_out * Lout) + 4.0 * L.C_in * L.C_out * L.k;
   const char* name = nullptr;
   ln.begin(flop, bytes);
   hipError_t e = L.prec == 1
@@ -1428,6 +1521,7 @@ int create_impl(const hfg_config* cfg, bool mrf_only, int device, hfg_handle** o
   if (const char* st = getenv("HFG_SMALL_TILE")) h->small_tile = atoi(st);
   if (const char* rc = getenv("HFG_RB_CONC")) h->rb_conc = atoi(rc);
   if (const char* us = getenv("HFG_UPS_SWIZZLE")) h->ups_swizzle = atoi(us);
+  if (const char* uf = getenv("HFG_UPS_FRAMES")) h->ups_frames = atoi(uf);
   if (const char* el = getenv("HFG_EPI_LDS")) h->epi_lds = atoi(el);
   if (const char* ar = getenv("HFG_AREG")) h->areg = atoi(ar) != 0;
   if (const char* se = getenv("HFG_SPLIT")) h->split = atoi(se);

@@ -154,6 +154,40 @@ hipError_t launch_conv_bf16x3(int tile, int kt, bool ups, int np, const ConvPara
                               int n_tiles, int m_tiles, int batch, hipStream_t stream,
                               const char** name);
 
+// ---- upsampler over output frames (ups_bf16x3.hip) ----
+// lrelu -> ConvTranspose1d(k = 2u, stride u, padding u/2) as a GEMM whose columns are the T
+// input frames: rows of class L (samples s < u/2 of a frame: taps x[m-1], x[m]) and class R
+// (s >= u/2: x[m], x[m+1]), both computed by every wave.  Bitwise the polyphase
+// conv1d_bf16x3 upsampler.
+struct UpsCfg {
+  int WAVES_M, WAVES_N, WM, WN;
+  constexpr int MT() const { return 32 * WM * WAVES_M; }  // rows per class and m-tile
+  constexpr int NTILE() const { return 32 * WN * WAVES_N; }
+  constexpr int threads() const { return 64 * WAVES_M * WAVES_N; }
+};
+// 0: 64 rows x 256 frames, 2x2 waves of 32 rows x 128 frames (x 2 classes)
+// 1: 32 rows x 256 frames, 1x4 waves of 32 x 64 (C_out * u / 2 = 32: V1 ups.3)
+constexpr int kUpsCfgs_n = 2;
+constexpr UpsCfg kUpsCfgs[kUpsCfgs_n] = {{2, 2, 1, 4}, {1, 4, 1, 2}};
+// rates whose two classes store whole runs: u = 2 (8 B), u = 4 (16 B), u/2 % 4 == 0 (16 B)
+inline constexpr bool ups_rate_ok(int u) { return u == 2 || u == 4 || (u % 8 == 0 && u > 0); }
+struct UpsParams {
+  const float* x;        // stage input [B][C_in][L]
+  int64_t x_bs;          // batch stride of x (C_in * L)
+  int C_in, L;           // channels, row length (L % 4 == 0)
+  int T;                 // frames (GEMM columns) per item, <= L
+  const int32_t* len_in; // per-item valid frames (device, [B]) or null = T
+  const __bf16* w;       // packed [m_tile][g][class][tap][plane][wave_m][wm][lane][8]
+  const float* bias;     // [C_out]
+  float* y;              // [B][C_out][L_out]
+  int64_t y_bs;
+  int C_out, L_out, u;
+  int m_tiles, n_tiles, batch;
+};
+size_t ups_lds_bytes(int cfg);
+hipError_t launch_ups_bf16x3(int cfg, int np, const UpsParams& p, hipStream_t stream,
+                             const char** name);
+
 // ---- whole ResBlock per launch (resblock_bf16x3.hip) ----
 // All 2*n_dil convs of one ResBlock of a C in {32, 64} stage on a window of
 // kRbColsPerWave * waves_n columns; x in registers, the conv operand in LDS.

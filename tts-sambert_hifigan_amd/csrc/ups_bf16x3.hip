@@ -1,0 +1,359 @@
+// ups_bf16x3.hip — the HiFi-GAN upsampler, lrelu -> ConvTranspose1d(C_in, C_out, k = 2u,
+// stride u, padding u/2) (models/hifigan.py:195-203, 244-245), as a split-precision
+// ("bf16x3") GEMM over OUTPUT FRAMES on the gfx950 bf16 matrix cores.
+//
+// Output sample t = m*u + s of frame m (s in [0, u), h = u/2) receives exactly two taps:
+//   class L (s <  h):  W[ci][co][s+h+u] * x[m-1]  +  W[ci][co][s+h] * x[m]
+//   class R (s >= h):  W[ci][co][s+h]   * x[m]    +  W[ci][co][s-h] * x[m+1]
+// so the GEMM columns are the T input frames themselves (no T+1 polyphase column and no
+// tail tile of one column), and every class has one block-uniform input offset per tap.
+// GEMM rows of a class: rr = co*h + s' (s' = s - class*h); a wave computes BOTH classes of
+// its rows and columns, so a lane ends up holding whole runs of consecutive samples:
+//   u = 2 (h = 1): (L, R) = samples 2m, 2m+1 of one channel        -> one 8-B store
+//   u = 4 (h = 2): rows (co,0),(co,1) x (L, R) = samples 4m..4m+3 -> one 16-B store
+//   h % 4 == 0:    4 consecutive rows = 4 consecutive samples      -> 16-B stores per class
+// (the polyphase kernel in conv_bf16x3.hip stores u = 2 stages one dword per value).
+//
+// Per output element the MFMA sequence is the polyphase kernel's (channel groups in order;
+// the x[m-1|m] tap before the x[m|m+1] tap; lo*hi, hi*lo, hi*hi), the split of lrelu(x) and
+// the zero padding are the same, the bias is added last: the result is bitwise equal to
+// conv1d_bf16x3<..., UPS> (tests/test_gpu_parity.py::test_ups_frames_kernel_bitwise).
+//
+// Data flow per 16-channel group g (one barrier per group):
+//   * A (weights): the host packs [m_tile][g][class][tap][plane][wave_m][wm][lane][8] bf16;
+//     the group's slab (128 * MT_c bf16) is copied to a 2-slot LDS ring by LDS-DMA one group
+//     ahead (no VGPRs).
+//   * B (lrelu'd, split input): the window of frames [m0-4, m0+NTILE+4) (quad-aligned, so
+//     every load is one 16-B dwordx4: 4 frames of one channel) is loaded one group ahead into
+//     registers, converted after the group's MFMAs and written as [frame][16 ch] bf16 hi / lo
+//     planes (16-B halves XOR-swizzled by (frame>>3)&1: conflict-free ds_read_b128 for the
+//     three tap offsets -1, 0, +1).
+#include <hip/hip_runtime.h>
+
+#include <mutex>
+
+#include <cstdio>
+
+#include "bf16x3_common.h"
+#include "kernels.h"
+
+namespace hfg {
+
+namespace {
+typedef float floatx2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+}  // namespace
+
+template <int WAVES_M, int WAVES_N, int WM, int WN, int NP>
+__global__ void __launch_bounds__(64 * WAVES_M * WAVES_N, 2)
+ups_bf16x3(const UpsParams p) {
+  constexpr int NW = WAVES_M * WAVES_N;
+  constexpr int NT = 64 * NW;
+  constexpr int MT = 32 * WM * WAVES_M;      // rows per class and m-tile
+  constexpr int NTILE = 32 * WN * WAVES_N;   // frames per block
+  constexpr int XR = NTILE + 8;              // staged frames: [m0 - 4, m0 + NTILE + 4)
+  constexpr int NQ = XR / 4;                 // frame quads
+  constexpr int NTASK = 2 * NQ;              // (quad, 8-channel half) staging tasks
+  constexpr int TPW = (NTASK + NW - 1) / NW; // tasks per wave (one per lane)
+  static_assert(TPW <= 64, "one staging task per lane");
+  constexpr int XPLANE = XR * 32;            // bytes per bf16 plane [frame][16 ch]
+  constexpr int XBUF = 2 * XPLANE;           // hi + lo
+  constexpr int SLAB = 2 * 2 * 2 * WAVES_M * WM * 1024;  // bytes: class x tap x plane x rows
+  constexpr int PW = SLAB / 1024 / NW;       // LDS-DMA pieces per thread per slab
+  static_assert(PW * 1024 * NW == SLAB, "slab must split evenly over the waves");
+
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  char* const Abuf = lds;                    // 2 slabs
+  char* const Xbuf = lds + 2 * SLAB;         // 2 x (hi, lo) planes
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wave_m = wave % WAVES_M;
+  const int wave_n = wave / WAVES_M;
+  const int half = lane >> 5;
+  const int col = lane & 31;
+
+  // block -> (m-tile fastest, frame tile, item), through an XCD swizzle: the m-tiles of one
+  // window run on one XCD (blocks b and b + 8 share an XCD under round-robin placement)
+  int mt, tx, b;
+  {
+    const int total = p.m_tiles * p.n_tiles * p.batch;
+    int id = blockIdx.x;
+    const int q = total >> 3;
+    if (id < (q << 3)) id = (id & 7) * q + (id >> 3);
+    mt = id % p.m_tiles;
+    id /= p.m_tiles;
+    tx = id % p.n_tiles;
+    b = id / p.n_tiles;
+    mt = __builtin_amdgcn_readfirstlane(mt);
+    tx = __builtin_amdgcn_readfirstlane(tx);
+    b = __builtin_amdgcn_readfirstlane(b);
+  }
+  const int T_b = p.len_in ? min(p.len_in[b], p.T) : p.T;
+  const int m0 = tx * NTILE;
+  if (m0 >= T_b) return;  // whole tile past this utterance's end (block-uniform)
+  const int NG = p.C_in / 16;
+
+  // ---- A slab ring: LDS-DMA, PW pieces per thread ----
+  const char* wsrc = reinterpret_cast<const char*>(p.w) + (int64_t)mt * NG * SLAB;
+  auto issue_a = [&](int g, int slot) {
+    const char* src = wsrc + (int64_t)g * SLAB;
+    char* dst = Abuf + slot * SLAB;
+#pragma unroll
+    for (int q = 0; q < PW; ++q) {
+      const int i = wave + q * NW;
+      __builtin_amdgcn_global_load_lds((gptr_t1)(src + i * 1024 + lane * 16),
+                                       (lds_ptr_t3)(dst + i * 1024), 16, 0, 0);
+    }
+  };
+
+  // ---- input staging: one (quad, half) task per lane of the first TPW lanes ----
+  // item-sized descriptor: a quad past the item's last row reads 0 (never faults)
+  const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(p.x + (int64_t)b * p.x_bs), 0, (int)((int64_t)p.C_in * p.L * 4), 0x00020000);
+  const int task = wave * TPW + lane;
+  const bool has_task = lane < TPW && task < NTASK;
+  const int hf = task / NQ;                  // channel half of the task
+  const int xq = task - hf * NQ;             // quad of the task
+  const int t0 = m0 - 4 + 4 * xq;            // first frame of the quad
+  // zero padding and leaky_relu as max(v * s1, v * s2): (1, 0.1) inside [0, T_b), (0, 0)
+  // outside (bitwise the polyphase kernel's staging)
+  float s1[4], s2[4];
+#pragma unroll
+  for (int tt = 0; tt < 4; ++tt) {
+    const bool ok = has_task && (unsigned)(t0 + tt) < (unsigned)T_b;
+    s1[tt] = ok ? 1.0f : 0.0f;
+    s2[tt] = ok ? kLReluSlope : 0.0f;
+  }
+  // whole quads only (L % 4 == 0, host-checked): a quad is inside the row or wholly outside
+  const bool q_in = has_task && t0 >= 0 && t0 < p.L;
+  const unsigned xoff_lane = q_in ? (unsigned)(8 * hf * p.L + t0) * 4u : 0u;
+  const int xcs4 = p.L * 4;
+  typedef float f4 __attribute__((ext_vector_type(4)));
+  f4 xv[8];
+  auto load_x = [&](int g) {
+    const unsigned o = xoff_lane + (q_in ? (unsigned)(g * 16) * (unsigned)xcs4 : 0u);
+#pragma unroll
+    for (int e = 0; e < 8; ++e)
+      xv[e] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(xrs, (int)o, e * xcs4, 0));
+  };
+  auto store_x = [&](int buf) {
+    if (!has_task) return;
+    char* xh = Xbuf + buf * XBUF;
+#pragma unroll
+    for (int tt = 0; tt < 4; ++tt) {
+      bf16x8 hv, lv;
+#pragma unroll
+      for (int e = 0; e < 8; e += 2) {
+        floatx2 a;
+        a[0] = fmaxf(xv[e][tt] * s1[tt], xv[e][tt] * s2[tt]);
+        a[1] = fmaxf(xv[e + 1][tt] * s1[tt], xv[e + 1][tt] * s2[tt]);
+        const bf16x2 hh = __builtin_convertvector(a, bf16x2);
+        const floatx2 hfl = __builtin_convertvector(hh, floatx2);
+        floatx2 d;
+        d[0] = a[0] - hfl[0];
+        d[1] = a[1] - hfl[1];
+        const bf16x2 ll = __builtin_convertvector(d, bf16x2);
+        hv[e] = hh[0];
+        hv[e + 1] = hh[1];
+        lv[e] = ll[0];
+        lv[e + 1] = ll[1];
+      }
+      const int r = 4 * xq + tt;
+      const int off = r * 32 + 16 * (hf ^ ((r >> 3) & 1));
+      *reinterpret_cast<bf16x8*>(xh + off) = hv;
+      *reinterpret_cast<bf16x8*>(xh + XPLANE + off) = lv;
+    }
+  };
+
+  floatx16 acc[2][WM][WN];
+#pragma unroll
+  for (int c = 0; c < 2; ++c)
+#pragma unroll
+    for (int i = 0; i < WM; ++i)
+#pragma unroll
+      for (int k = 0; k < WN; ++k)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[c][i][k][r] = 0.f;
+
+  // ---- prologue: group 0 ----
+  issue_a(0, 0);
+  load_x(0);
+  store_x(0);
+  wait_vm<0>();
+  lds_barrier();
+
+  // B fragment rows: window row of frame m0 + colw is colw + 4
+  const int colw = wave_n * 32 * WN + col + 4;
+  for (int g = 0; g < NG; ++g) {
+    const bool more = g + 1 < NG;  // block-uniform
+    if (more) {
+      issue_a(g + 1, (g + 1) & 1);
+      load_x(g + 1);
+    }
+    // A fragments of both classes and taps: [class][tap][plane][wm]
+    const char* as = Abuf + (g & 1) * SLAB;
+    bf16x8 a[2][2][2][WM];
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int tp = 0; tp < 2; ++tp)
+#pragma unroll
+        for (int pl = 0; pl < 2; ++pl)
+#pragma unroll
+          for (int i = 0; i < WM; ++i)
+            a[c][tp][pl][i] = *reinterpret_cast<const bf16x8*>(
+                as + ((((c * 2 + tp) * 2 + pl) * WAVES_M + wave_m) * WM + i) * 1024 + lane * 16);
+    const char* xh = Xbuf + (g & 1) * XBUF;
+#pragma unroll
+    for (int k = 0; k < WN; ++k) {
+      // B at tap offsets -1, 0, +1 (hi, lo)
+      bf16x8 bh[3], bl[3];
+#pragma unroll
+      for (int o = 0; o < 3; ++o) {
+        const int r = colw + 32 * k + o - 1;
+        const int off = r * 32 + 16 * (half ^ ((r >> 3) & 1));
+        bh[o] = *reinterpret_cast<const bf16x8*>(xh + off);
+        bl[o] = *reinterpret_cast<const bf16x8*>(xh + XPLANE + off);
+      }
+#pragma unroll
+      for (int i = 0; i < WM; ++i)
+#pragma unroll
+        for (int c = 0; c < 2; ++c)
+#pragma unroll
+          for (int tp = 0; tp < 2; ++tp) {
+            const int o = c + tp;  // class L: offsets -1, 0 (o = 0, 1); class R: 0, +1 (1, 2)
+            if constexpr (NP == 3)
+              acc[c][i][k] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[c][tp][1][i], bh[o],
+                                                                    acc[c][i][k], 0, 0, 0);
+            acc[c][i][k] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[c][tp][0][i], bl[o],
+                                                                  acc[c][i][k], 0, 0, 0);
+            acc[c][i][k] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[c][tp][0][i], bh[o],
+                                                                  acc[c][i][k], 0, 0, 0);
+          }
+    }
+    if (more) store_x((g + 1) & 1);
+    wait_vm<0>();
+    lds_barrier();
+  }
+
+  // ---- epilogue: bias, stores of whole sample runs ----
+  float* yb = p.y + (int64_t)b * p.y_bs;
+  const int h = p.u >> 1;
+#pragma unroll
+  for (int i = 0; i < WM; ++i) {
+    const int rb = mt * MT + wave_m * 32 * WM + i * 32 + 4 * half;  // row of r = 0
+#pragma unroll
+    for (int k = 0; k < WN; ++k) {
+      const int m = m0 + wave_n * 32 * WN + k * 32 + col;
+      if (m >= T_b) continue;
+      if (h == 1) {
+        // rows = channels: (L, R) = samples 2m, 2m + 1
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int co = rb + (r & 3) + 8 * (r >> 2);
+          const float bv = p.bias[co];
+          floatx2 v;
+          v[0] = acc[0][i][k][r] + bv;
+          v[1] = acc[1][i][k][r] + bv;
+          *reinterpret_cast<floatx2*>(yb + (int64_t)co * p.L_out + 2 * m) = v;
+        }
+      } else if (h == 2) {
+        // rows (co, 0), (co, 1), (co + 1, 0), (co + 1, 1): samples 4m .. 4m + 3 of co, co + 1
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+#pragma unroll
+          for (int pr = 0; pr < 2; ++pr) {
+            const int r0 = 4 * q + 2 * pr;
+            const int co = (rb + 8 * q + 2 * pr) >> 1;
+            const float bv = p.bias[co];
+            float4 v;
+            v.x = acc[0][i][k][r0] + bv;
+            v.y = acc[0][i][k][r0 + 1] + bv;
+            v.z = acc[1][i][k][r0] + bv;
+            v.w = acc[1][i][k][r0 + 1] + bv;
+            *reinterpret_cast<float4*>(yb + (int64_t)co * p.L_out + 4 * m) = v;
+          }
+      } else {
+        // h % 4 == 0: 4 consecutive rows = s' .. s' + 3 of one channel, per class
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int row = rb + 8 * q;
+          const int co = row / h, sp = row - co * h;
+          const float bv = p.bias[co];
+#pragma unroll
+          for (int c = 0; c < 2; ++c) {
+            float4 v;
+            v.x = acc[c][i][k][4 * q + 0] + bv;
+            v.y = acc[c][i][k][4 * q + 1] + bv;
+            v.z = acc[c][i][k][4 * q + 2] + bv;
+            v.w = acc[c][i][k][4 * q + 3] + bv;
+            *reinterpret_cast<float4*>(yb + (int64_t)co * p.L_out + m * p.u + c * h + sp) = v;
+          }
+        }
+      }
+    }
+  }
+}
+
+namespace {
+
+typedef void (*UpsFn)(const UpsParams);
+
+struct EntryUps {
+  int cfg, np;
+  UpsFn fn;
+  char name[64];
+};
+
+#define HFGUPS_ENTRY(CFG, NP)                                                                \
+  {                                                                                          \
+    CFG, NP,                                                                                 \
+        ups_bf16x3<kUpsCfgs[CFG].WAVES_M, kUpsCfgs[CFG].WAVES_N, kUpsCfgs[CFG].WM,          \
+                   kUpsCfgs[CFG].WN, NP>,                                                    \
+    {                                                                                        \
+      0                                                                                      \
+    }                                                                                        \
+  }
+
+EntryUps g_entriesUps[] = {HFGUPS_ENTRY(0, 3), HFGUPS_ENTRY(1, 3), HFGUPS_ENTRY(0, 2),
+                           HFGUPS_ENTRY(1, 2)};
+
+}  // namespace
+
+size_t ups_lds_bytes(int cfg) {
+  const UpsCfg& t = kUpsCfgs[cfg];
+  const size_t slab = (size_t)2 * 2 * 2 * t.WAVES_M * t.WM * 1024;
+  const size_t xr = (size_t)t.NTILE() + 8;
+  return 2 * slab + 2 * 2 * xr * 32;
+}
+
+hipError_t launch_ups_bf16x3(int cfg, int np, const UpsParams& p, hipStream_t stream,
+                             const char** name) {
+  EntryUps* e = nullptr;
+  for (auto& cand : g_entriesUps)
+    if (cand.cfg == cfg && cand.np == np) e = &cand;
+  if (!e) return hipErrorInvalidValue;
+  const UpsCfg& t = kUpsCfgs[cfg];
+  // shapes the kernel's indexing assumes
+  if (p.C_in % 16 != 0 || p.L % 4 != 0 || p.T > p.L || p.u < 2 || (p.u & 1) ||
+      !ups_rate_ok(p.u) || p.L_out < p.L * p.u || p.m_tiles * t.MT() * 2 != p.C_out * p.u ||
+      p.n_tiles * t.NTILE() < p.T || (int64_t)p.C_in * p.L * 4 >= ((int64_t)1 << 31))
+    return hipErrorInvalidValue;
+  {
+    std::lock_guard<std::mutex> lk(setup_mutex());
+    if (!e->name[0])
+      snprintf(e->name, sizeof(e->name), "ups_bf16x3<%d, %d, %d, %d, %d>", t.WAVES_M, t.WAVES_N,
+               t.WM, t.WN, np);
+  }
+  const size_t lds = ups_lds_bytes(cfg);
+  if (lds > 160 * 1024) return hipErrorInvalidValue;
+  if (hipError_t err = ensure_max_lds(reinterpret_cast<const void*>(e->fn))) return err;
+  if (name) *name = e->name;
+  const int blocks = p.m_tiles * p.n_tiles * p.batch;
+  e->fn<<<dim3(blocks), dim3(t.threads()), lds, stream>>>(p);
+  return hipGetLastError();
+}
+
+}  // namespace hfg
