@@ -1118,7 +1118,8 @@ int run_ups(hfg_handle* h, Launcher& ln, const Layer& L, const float* x, int64_t
   if (L.ups_cfg >= 0 && h->ups_frames && Lin % 4 == 0 && Lout == Lin * L.s) {
     // output-frame kernel, unless its grid would leave most CUs idle (then the polyphase
     // kernel's small-grid tile): bitwise the same result either way
-    const hfg::UpsCfg& t = hfg::kUpsCfgs[L.ups_cfg];
+    const int cfg = L.ups_cfg;
+    const hfg::UpsCfg& t = hfg::kUpsCfgs[cfg];
     const int n_tiles = (int)((Lin + t.NTILE() - 1) / t.NTILE());
     if (h->ups_frames == 2 ||
         (int64_t)L.m_tiles_f * n_tiles * B * ln.conc >= hfg::kSmallGridBlocks) {
@@ -1139,9 +1140,10 @@ int run_ups(hfg_handle* h, Launcher& ln, const Layer& L, const float* x, int64_t
       q.m_tiles = L.m_tiles_f;
       q.n_tiles = n_tiles;
       q.batch = (int)B;
+      q.dbg = h->dbg_flags;
       const char* name = nullptr;
       ln.begin(flop, bytes);
-      hipError_t e = hfg::launch_ups_bf16x3(L.ups_cfg, h->np, q, ln.stream, &name);
+      hipError_t e = hfg::launch_ups_bf16x3(cfg, h->np, q, ln.stream, &name);
       ln.end(name);
       if (e != hipSuccess)
         return fail(HFG_EIO, "launch %s: %s", L.mod.c_str(), hipGetErrorString(e));

@@ -167,6 +167,8 @@ struct UpsCfg {
 };
 // 0: 64 rows x 256 frames, 2x2 waves of 32 rows x 128 frames (x 2 classes)
 // 1: 32 rows x 256 frames, 1x4 waves of 32 x 64 (C_out * u / 2 = 32: V1 ups.3)
+// (128-frame tiles of both, 3 blocks per CU, measured 30 % slower on ups.2 / 8 % on ups.3
+// and 2x on ups.0 + ups.1: profiles/r03/ups/nt_ab.txt)
 constexpr int kUpsCfgs_n = 2;
 constexpr UpsCfg kUpsCfgs[kUpsCfgs_n] = {{2, 2, 1, 4}, {1, 4, 1, 2}};
 // rates whose two classes store whole runs: u = 2 (8 B), u = 4 (16 B), u/2 % 4 == 0 (16 B)
@@ -183,6 +185,8 @@ struct UpsParams {
   int64_t y_bs;
   int C_out, L_out, u;
   int m_tiles, n_tiles, batch;
+  int dbg;               // ablations (HFG_DEBUG_FLAGS, timing only, wrong results): bit9 no
+                         // input conversion after group 0, bit10 no input loads after group 0
 };
 size_t ups_lds_bytes(int cfg);
 hipError_t launch_ups_bf16x3(int cfg, int np, const UpsParams& p, hipStream_t stream,

@@ -37,6 +37,11 @@
 #include "bf16x3_common.h"
 #include "kernels.h"
 
+// u = 2 epilogue: 16-B stores through a DPP pair swap (1) or 8-B stores (0)
+#ifndef HFG_UPS_PAIR
+#define HFG_UPS_PAIR 1
+#endif
+
 namespace hfg {
 
 namespace {
@@ -190,7 +195,7 @@ ups_bf16x3(const UpsParams p) {
     const bool more = g + 1 < NG;  // block-uniform
     if (more) {
       issue_a(g + 1, (g + 1) & 1);
-      load_x(g + 1);
+      if (!(p.dbg & 1024)) load_x(g + 1);
     }
     // A fragments of both classes and taps: [class][tap][plane][wm]
     const char* as = Abuf + (g & 1) * SLAB;
@@ -233,7 +238,7 @@ ups_bf16x3(const UpsParams p) {
                                                                   acc[c][i][k], 0, 0, 0);
           }
     }
-    if (more) store_x((g + 1) & 1);
+    if (more && !(p.dbg & 512)) store_x((g + 1) & 1);
     wait_vm<0>();
     lds_barrier();
   }
@@ -248,7 +253,45 @@ ups_bf16x3(const UpsParams p) {
     for (int k = 0; k < WN; ++k) {
       const int m = m0 + wave_n * 32 * WN + k * 32 + col;
       if (m >= T_b) continue;
-      if (h == 1) {
+      if (h == 1 && HFG_UPS_PAIR) {
+        // rows = channels: (L, R) = samples 2m, 2m + 1.  Adjacent lanes (frames m, m + 1,
+        // m even) swap one channel's pair (DPP quad_perm [1,0,3,2]): the even lane then
+        // holds samples 2m .. 2m + 3 of channel r, the odd lane those of channel r + 1 ->
+        // one 16-B store per lane and channel pair instead of two 8-B stores
+        const bool odd = col & 1;
+        const int me = m - (odd ? 1 : 0);  // even frame of the pair
+        const bool quad_ok = me + 1 < T_b;
+#pragma unroll
+        for (int r = 0; r < 16; r += 2) {
+          const int co0 = rb + (r & 3) + 8 * (r >> 2);
+          const float b0 = p.bias[co0], b1 = p.bias[co0 + 1];
+          const float l0 = acc[0][i][k][r] + b0, r0 = acc[1][i][k][r] + b0;
+          const float l1 = acc[0][i][k][r + 1] + b1, r1 = acc[1][i][k][r + 1] + b1;
+          const float s0 = odd ? l0 : l1, s1 = odd ? r0 : r1;
+          const float v0 = __builtin_bit_cast(
+              float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, s0), 0xB1, 0xF, 0xF, false));
+          const float v1 = __builtin_bit_cast(
+              float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, s1), 0xB1, 0xF, 0xF, false));
+          if (quad_ok) {
+            float4 v;
+            v.x = odd ? v0 : l0;
+            v.y = odd ? v1 : r0;
+            v.z = odd ? l1 : v0;
+            v.w = odd ? r1 : v1;
+            *reinterpret_cast<float4*>(yb + (int64_t)(odd ? co0 + 1 : co0) * p.L_out + 2 * me) = v;
+          } else {
+            // last frame of an odd-length utterance (even lane, its odd partner past T_b):
+            // both channels' pairs as 8-B stores
+            floatx2 a, c;
+            a[0] = l0;
+            a[1] = r0;
+            c[0] = l1;
+            c[1] = r1;
+            *reinterpret_cast<floatx2*>(yb + (int64_t)co0 * p.L_out + 2 * m) = a;
+            *reinterpret_cast<floatx2*>(yb + (int64_t)(co0 + 1) * p.L_out + 2 * m) = c;
+          }
+        }
+      } else if (h == 1) {
         // rows = channels: (L, R) = samples 2m, 2m + 1
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
