@@ -53,7 +53,6 @@ template <int WAVES_M, int WAVES_N, int WM, int WN, int NP>
 __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N, 2)
 ups_bf16x3(const UpsParams p) {
   constexpr int NW = WAVES_M * WAVES_N;
-  constexpr int NT = 64 * NW;
   constexpr int MT = 32 * WM * WAVES_M;      // rows per class and m-tile
   constexpr int NTILE = 32 * WN * WAVES_N;   // frames per block
   constexpr int XR = NTILE + 8;              // staged frames: [m0 - 4, m0 + NTILE + 4)
@@ -114,9 +113,12 @@ ups_bf16x3(const UpsParams p) {
   };
 
   // ---- input staging: one (quad, half) task per lane of the first TPW lanes ----
-  // item-sized descriptor: a quad past the item's last row reads 0 (never faults)
+  // item-sized descriptor: a quad past the item's last row reads 0 (never faults).  An item
+  // holds at most 2^30 floats (host-checked): byte offsets and the range fit 32 bits
+  const int64_t item_bytes = (int64_t)p.C_in * p.L * 4;
   const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)(p.x + (int64_t)b * p.x_bs), 0, (int)((int64_t)p.C_in * p.L * 4), 0x00020000);
+      (void*)(p.x + (int64_t)b * p.x_bs), 0,
+      (int)(unsigned)(item_bytes < 0xFFFFFFFFll ? item_bytes : 0xFFFFFFFFll), 0x00020000);
   const int task = wave * TPW + lane;
   const bool has_task = lane < TPW && task < NTASK;
   const int hf = task / NQ;                  // channel half of the task
@@ -382,7 +384,7 @@ hipError_t launch_ups_bf16x3(int cfg, int np, const UpsParams& p, hipStream_t st
   // shapes the kernel's indexing assumes
   if (p.C_in % 16 != 0 || p.L % 4 != 0 || p.T > p.L || p.u < 2 || (p.u & 1) ||
       !ups_rate_ok(p.u) || p.L_out < p.L * p.u || p.m_tiles * t.MT() * 2 != p.C_out * p.u ||
-      p.n_tiles * t.NTILE() < p.T || (int64_t)p.C_in * p.L * 4 >= ((int64_t)1 << 31))
+      p.n_tiles * t.NTILE() < p.T || (int64_t)p.C_in * p.L > ((int64_t)1 << 30))
     return hipErrorInvalidValue;
   {
     std::lock_guard<std::mutex> lk(setup_mutex());
