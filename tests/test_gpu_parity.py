@@ -211,17 +211,22 @@ def test_bf16x3_layer_kernels_run_to_run_bitwise(pkg, big_tile, fused, monkeypat
 @pytest.mark.parametrize("precision", ["bf16x3", "bf16w"])
 @pytest.mark.parametrize("preset,B,T,lens", [("v1", 3, 64, [64, 41, 3]),
                                              ("v2star", 2, 64, [64, 17]),
-                                             ("nonexact", 2, 64, [64, 29])])
+                                             ("nonexact", 2, 64, [64, 29]),
+                                             ("rates248", 3, 36, [36, 21, 5])])
 def test_ups_frames_kernel_bitwise(pkg, preset, B, T, lens, precision, monkeypatch):
     """The output-frame upsampler kernel (csrc/ups_bf16x3.hip: k = 2u stages, both sample
     classes of a frame per wave) gives the polyphase conv1d_bf16x3 upsampler's result bit
     for bit: the same MFMA sequence per output element, the same split of lrelu(x), the
     same zero padding.  HFG_UPS_FRAMES=2 forces it onto every eligible stage (rates 8 and 2
     in V1 / V2*, 4 and 2 in the non-exact preset; rate 5 stays polyphase), 0 keeps the
-    polyphase kernel; ragged and full batches."""
+    polyphase kernel; ragged and full batches.  "rates248" puts the rate-2 stage first, so
+    a ragged item has an odd number of input frames there (the DPP-paired 16-B store's
+    last-frame path)."""
     from oracle import config as C, prng
     dev = _dev()
-    cfg = C.PRESETS[preset]
+    cfg = C.PRESETS.get(preset) or C.GenConfig(
+        upsample_rates=[2, 4, 8], upsample_kernel_sizes=[4, 8, 16], upsample_initial_channel=256,
+        resblock_kernel_sizes=[3, 5], resblock_dilation_sizes=[[1, 3], [1]])
     sd = C.make_state_dict(cfg, seed=31)
     mel = torch.as_tensor(prng.mel_input(31 + T, (B, cfg.n_mels, T))).to(dev)
     ln = torch.tensor(lens, dtype=torch.int32, device=dev)
