@@ -245,3 +245,33 @@ def test_ups_frames_kernel_bitwise(pkg, preset, B, T, lens, precision, monkeypat
     assert "ups_bf16x3<" in names["2"] and "ups_bf16x3<" not in names["0"], names
     for a, b in zip(outs["0"], outs["2"]):
         assert np.array_equal(a, b), np.abs(a - b).max()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("precision", ["bf16x3", "fp32"])
+def test_conv_post_quad_kernel_bitwise(pkg, precision, monkeypatch):
+    """conv_post4_tanh (4 samples per thread, no LDS) gives the LDS-staged conv_post_tanh's
+    wav bit for bit — the same (channel, tap) fma order per sample — on a ragged batch whose
+    lengths end inside a 4-sample quad and a window edge (HFG_POST4=0 keeps the old kernel)."""
+    from oracle import config as C, prng
+    dev = _dev()
+    cfg = C.V1
+    sd = C.make_state_dict(cfg, seed=41)
+    mel = torch.as_tensor(prng.mel_input(41, (3, cfg.n_mels, 40))).to(dev)
+    ln = torch.tensor([40, 17, 1], dtype=torch.int32, device=dev)
+    outs, names = {}, {}
+    for mode in ("0", "1"):
+        monkeypatch.setenv("HFG_POST4", mode)
+        gen = _gen(pkg, cfg, sd, dev, precision=precision)
+        h = gen.hip_handle(dev)
+        h.profile_reset()
+        h.set_profiling(True)
+        with torch.no_grad():
+            outs[mode] = (gen(mel).cpu().numpy(), gen(mel, lengths=ln).cpu().numpy())
+        torch.cuda.synchronize()
+        h.set_profiling(False)
+        names[mode] = " ".join(h.profile_summary())
+    assert "conv_post4_tanh" in names["1"] and "conv_post4_tanh" not in names["0"], names
+    for a, b in zip(outs["0"], outs["1"]):
+        assert np.array_equal(a, b), np.abs(a - b).max()
+    assert not outs["1"][1][1, :, 17 * 256:].any() and not outs["1"][1][2, :, 256:].any()

@@ -302,6 +302,68 @@ conv_post_tanh(const float* __restrict__ x, int64_t x_bs, int C, int L, const fl
   wav[(int64_t)b * L + t] = t >= Lb ? 0.f : tanhf(acc + bias[0]);
 }
 
+// conv_post + tanh for L % 4 == 0 (every V1 / V2* wav): four consecutive samples per
+// thread, no LDS and no barrier.  Per channel a thread reads the 16-B quads at t - 4, t and
+// t + 4 (its neighbours' quads: the same cache lines, so HBM bytes stay one pass over x),
+// eight channels' loads in flight at a time; quads outside the row read offset 0 (masked).  Per output the sum runs over (channel, tap) in the order conv_post_tanh
+// uses (channel-major, fma from 0, bias last): bitwise its result.
+__global__ void __launch_bounds__(256)
+conv_post4_tanh(const float* __restrict__ x, int64_t x_bs, int C, int L, const float* __restrict__ w,
+                const float* __restrict__ bias, float* __restrict__ wav,
+                const int32_t* __restrict__ lens) {
+  constexpr int KP = 7, CB = 8;
+  typedef float f4 __attribute__((ext_vector_type(4)));
+  const int b = blockIdx.y;
+  const int t = (blockIdx.x * 256 + threadIdx.x) * 4;  // first of this thread's 4 samples
+  if (t >= L) return;
+  const int Lb = lens ? min(lens[b], L) : L;
+  float* out = wav + (int64_t)b * L + t;
+  if (t >= Lb) {  // past this utterance's end: zeros
+    *reinterpret_cast<f4*>(out) = f4{0.f, 0.f, 0.f, 0.f};
+    return;
+  }
+  // an item holds at most 2^30 floats: byte offsets from the item base fit 32 bits (a
+  // buffer descriptor cannot: a 4-GiB item's range does not fit its 32-bit record count)
+  const char* xb = reinterpret_cast<const char*>(x + (int64_t)b * x_bs);
+  // the three quads [t-4, t), [t, t+4), [t+4, t+8); element k of v = x[t - 4 + k]
+  const bool okq[3] = {t - 4 >= 0, true, t + 4 < L};
+  bool okv[12];
+#pragma unroll
+  for (int k = 0; k < 12; ++k) okv[k] = (unsigned)(t - 4 + k) < (unsigned)Lb;
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  for (int c0 = 0; c0 < C; c0 += CB) {
+    f4 q[CB][3];
+#pragma unroll
+    for (int e = 0; e < CB; ++e) {
+      const int c = min(c0 + e, C - 1);
+#pragma unroll
+      for (int s = 0; s < 3; ++s) {
+        const unsigned off = okq[s] ? (unsigned)(c * L + t - 4 + 4 * s) * 4u : 0u;
+        q[e][s] = *reinterpret_cast<const f4*>(xb + off);
+      }
+    }
+#pragma unroll
+    for (int e = 0; e < CB; ++e) {
+      if (c0 + e >= C) break;
+      float v[12];
+#pragma unroll
+      for (int k = 0; k < 12; ++k) {
+        const float r = q[e][k >> 2][k & 3];
+        v[k] = okv[k] ? lrelu(r) : 0.f;
+      }
+      const float* ws = w + (c0 + e) * KP;
+#pragma unroll
+      for (int o = 0; o < 4; ++o)
+#pragma unroll
+        for (int j = 0; j < KP; ++j) acc[o] = fmaf(ws[j], v[o + j + 1], acc[o]);
+    }
+  }
+  f4 r;
+#pragma unroll
+  for (int o = 0; o < 4; ++o) r[o] = t + o >= Lb ? 0.f : tanhf(acc[o] + bias[0]);
+  *reinterpret_cast<f4*>(out) = r;
+}
+
 // ------------------------------------------------------------------------
 // dispatch
 // ------------------------------------------------------------------------
@@ -377,7 +439,13 @@ hipError_t launch_conv(TileId tile, int kt, bool ups, const ConvParams& p, int n
 
 hipError_t launch_conv_post(const float* x, int64_t x_bs, int C, int L, const float* w,
                             const float* bias, float* wav, const int32_t* lens, int batch,
-                            hipStream_t stream, const char** name) {
+                            hipStream_t stream, const char** name, bool quad) {
+  if (quad && conv_post4_ok(L) && (int64_t)C * L <= ((int64_t)1 << 30)) {
+    if (name) *name = "conv_post4_tanh";
+    dim3 grid((L / 4 + 255) / 256, batch);
+    conv_post4_tanh<<<grid, dim3(256), 0, stream>>>(x, x_bs, C, L, w, bias, wav, lens);
+    return hipGetLastError();
+  }
   const size_t lds = conv_post_lds_bytes(C);
   if (lds > 160 * 1024) return hipErrorInvalidValue;
   if (hipError_t err = ensure_max_lds(reinterpret_cast<const void*>(conv_post_tanh)))

@@ -171,6 +171,8 @@ struct hfg_handle {
                              // (HFG_RB_WN32: 4 or 8)
   bool mfma16 = true;        // 16x16x32-shape ResBlock kernel for C = 32 (HFG_MFMA16=0: off)
   int ups_swizzle = 1;       // XCD swizzle of the upsampler blocks (HFG_UPS_SWIZZLE=0: off)
+  bool post4 = true;         // conv_post on the 4-samples-per-thread kernel where L % 4 == 0
+                             // (HFG_POST4=0: the LDS-staged kernel; bitwise the same wav)
   int ups_frames = 1;        // k = 2u upsamplers on the output-frame kernel: 1 when its grid
                              // fills the chip, 2 always, 0 never (HFG_UPS_FRAMES; the
                              // polyphase conv1d_bf16x3 path gives the bitwise same result)
@@ -1450,7 +1452,7 @@ int forward_impl(hfg_handle* h, const float* mel, int64_t B, int64_t T, const hf
     ln.begin(2.0 * Lp.C_in * 7 * (double)L * B, 4.0 * B * L * (Lp.C_in + 1));
     hipError_t e = hfg::launch_conv_post(cur, (int64_t)Lp.C_in * L, Lp.C_in, (int)L,
                                          h->packed_dev + Lp.w_off, h->packed_dev + Lp.b_off, wav,
-                                         lens_at(c.n_up), (int)B, stream, &name);
+                                         lens_at(c.n_up), (int)B, stream, &name, h->post4);
     ln.end(name);
     if (e != hipSuccess) return fail(HFG_EIO, "launch conv_post: %s", hipGetErrorString(e));
   }
@@ -1524,6 +1526,7 @@ int create_impl(const hfg_config* cfg, bool mrf_only, int device, hfg_handle** o
   if (const char* rc = getenv("HFG_RB_CONC")) h->rb_conc = atoi(rc);
   if (const char* us = getenv("HFG_UPS_SWIZZLE")) h->ups_swizzle = atoi(us);
   if (const char* uf = getenv("HFG_UPS_FRAMES")) h->ups_frames = atoi(uf);
+  if (const char* pq = getenv("HFG_POST4")) h->post4 = atoi(pq) != 0;
   if (const char* el = getenv("HFG_EPI_LDS")) h->epi_lds = atoi(el);
   if (const char* ar = getenv("HFG_AREG")) h->areg = atoi(ar) != 0;
   if (const char* se = getenv("HFG_SPLIT")) h->split = atoi(se);

@@ -296,10 +296,12 @@ inline size_t conv_post_lds_bytes(int C) {
   return sizeof(float) * ((size_t)((C * 7 + 3) & ~3) + (size_t)(C < kConvPostCB ? C : kConvPostCB) * (256 + 6));
 }
 // conv_post + tanh: wav[b][t] = tanh(bias + sum_{c,j} w[c][j] * lrelu(x[b][c][t+j-3]))
-// for t < lens[b] (lens null = L); 0 beyond.
+// for t < lens[b] (lens null = L); 0 beyond.  quad: the 4-samples-per-thread kernel
+// (conv_post4_tanh) where L % 4 == 0 — bitwise the LDS-staged one.
+inline bool conv_post4_ok(int L) { return L % 4 == 0; }
 hipError_t launch_conv_post(const float* x, int64_t x_bs, int C, int L, const float* w,
                             const float* bias, float* wav, const int32_t* lens, int batch,
-                            hipStream_t stream, const char** name);
+                            hipStream_t stream, const char** name, bool quad = true);
 
 // Content hash of up to kChecksumMax fp32 tensors per launch: out[base + i] +=
 // sum_w mix(word_w, w) over tensor i's n[i] 32-bit words (out zeroed by the caller).

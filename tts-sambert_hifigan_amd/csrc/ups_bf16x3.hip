@@ -113,12 +113,11 @@ ups_bf16x3(const UpsParams p) {
   };
 
   // ---- input staging: one (quad, half) task per lane of the first TPW lanes ----
-  // item-sized descriptor: a quad past the item's last row reads 0 (never faults).  An item
-  // holds at most 2^30 floats (host-checked): byte offsets and the range fit 32 bits
-  const int64_t item_bytes = (int64_t)p.C_in * p.L * 4;
-  const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)(p.x + (int64_t)b * p.x_bs), 0,
-      (int)(unsigned)(item_bytes < 0xFFFFFFFFll ? item_bytes : 0xFFFFFFFFll), 0x00020000);
+  // one buffer descriptor per 16-channel group (SGPR base + record count: a whole 4-GiB
+  // item would not fit the 32-bit count); a quad outside its row reads offset 0 (masked)
+  const char* xb = reinterpret_cast<const char*>(p.x + (int64_t)b * p.x_bs);
+  const int64_t grp_bytes = (int64_t)16 * p.L * 4;
+  const int grp_rec = (int)(unsigned)(grp_bytes < 0xFFFFFFFFll ? grp_bytes : 0xFFFFFFFFll);
   const int task = wave * TPW + lane;
   const bool has_task = lane < TPW && task < NTASK;
   const int hf = task / NQ;                  // channel half of the task
@@ -140,10 +139,12 @@ ups_bf16x3(const UpsParams p) {
   typedef float f4 __attribute__((ext_vector_type(4)));
   f4 xv[8];
   auto load_x = [&](int g) {
-    const unsigned o = xoff_lane + (q_in ? (unsigned)(g * 16) * (unsigned)xcs4 : 0u);
+    const __amdgpu_buffer_rsrc_t xrs =
+        __builtin_amdgcn_make_buffer_rsrc((void*)(xb + g * grp_bytes), 0, grp_rec, 0x00020000);
 #pragma unroll
     for (int e = 0; e < 8; ++e)
-      xv[e] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(xrs, (int)o, e * xcs4, 0));
+      xv[e] = __builtin_bit_cast(
+          f4, __builtin_amdgcn_raw_buffer_load_b128(xrs, (int)xoff_lane, e * xcs4, 0));
   };
   auto store_x = [&](int buf) {
     if (!has_task) return;
