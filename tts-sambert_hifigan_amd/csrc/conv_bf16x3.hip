@@ -34,6 +34,18 @@
 #ifndef HFG_AREG_AD
 #define HFG_AREG_AD 2
 #endif
+// tile-5 tap schedule: the next group's input loads issue at tap KT - HFG_AREG_XT; VALU
+// fillers per MFMA on the plain taps (HFG_AREG_NV) and on the last (store) tap
+// (HFG_AREG_NVST)
+#ifndef HFG_AREG_XT
+#define HFG_AREG_XT 4
+#endif
+#ifndef HFG_AREG_NV
+#define HFG_AREG_NV 2
+#endif
+#ifndef HFG_AREG_NVST
+#define HFG_AREG_NVST 6
+#endif
 
 namespace hfg {
 
@@ -380,11 +392,12 @@ conv1d_bf16x3(const ConvParams p) {
     constexpr int KT = KT_;
     constexpr int NTG = (KT + TPC - 1) / TPC;
     constexpr int AD = HFG_AREG_AD;           // A prefetch distance in taps (1 or 2)
-    constexpr int XT = KT >= 4 ? KT - 4 : 0;  // tap issuing the next group's input loads
+    constexpr int XT = KT >= HFG_AREG_XT ? KT - HFG_AREG_XT : 0;  // tap issuing the next
+                                                                  // group's input loads
     static_assert(AD <= KT && XT < KT - 1, "AREG schedule");
     using I0 = std::integral_constant<int, 0>;
-    using I2 = std::integral_constant<int, 2>;
-    using I6 = std::integral_constant<int, 6>;
+    using I2 = std::integral_constant<int, HFG_AREG_NV>;
+    using I6 = std::integral_constant<int, HFG_AREG_NVST>;
     using T_ = std::true_type;
     using F_ = std::false_type;
     const int NG = p.n_chunks / NTG;
