@@ -6,7 +6,7 @@ set -e
 NAME=$1; SRCS=$2; shift 2
 P=tts-sambert_hifigan_amd; B=$P/build; V=/tmp/variant_$NAME; mkdir -p $V
 OBJS=""
-for o in conv_kernels conv_bf16x3 resblock_bf16x3 resblock16_bf16x3 mrf_thin mrf_thin_mfma ups_bf16x3 probe hifigan_capi mel_kernels mel_capi; do
+for o in conv_kernels conv_bf16x3 resblock_bf16x3 mrf_thin mrf_thin_mfma ups_bf16x3 probe hifigan_capi mel_kernels mel_capi; do
   if [[ " $SRCS " == *" $o.hip "* || " $SRCS " == *" $o.cpp "* ]]; then
     src=$P/csrc/$o.hip; [ -f $src ] || src=$P/csrc/$o.cpp
     /opt/rocm/bin/hipcc --offload-arch=gfx950 -mcode-object-version=5 -O3 -std=c++17 -fPIC -Wall \

@@ -330,14 +330,12 @@ def _conv_same(x, w, b, d):
     return out
 
 
-@pytest.mark.parametrize("m16", ["1", "0"])
 @pytest.mark.parametrize("preset", ["v1", "v2star"])
-def test_resblock_stream_packing_and_windowing(pkg, preset, m16, monkeypatch):
+def test_resblock_stream_packing_and_windowing(pkg, preset):
     """Whole-ResBlock launches (resblock_bf16x3.hip) of the narrow stages: the packed A
     stream decodes (hi + lo, permuted channel slots) to every conv's weights, and the
     kernel's windowing (NWIN-column windows, garbage edges, centre W = NWIN - 2*halo,
     zero outside [0, len)) reproduces the un-windowed ResBlock, emulated in float64."""
-    monkeypatch.setenv("HFG_MFMA16", m16)
     cfg = C.PRESETS[preset]
     sd = C.make_state_dict(cfg, seed=43)
     h = host_handle(pkg, cfg, "bf16x3")
@@ -353,7 +351,7 @@ def test_resblock_stream_packing_and_windowing(pkg, preset, m16, monkeypatch):
                 assert Cst not in (32, 64) or preset != "v1"
                 continue
             n_fused += 1
-            assert info["fused"] == (2 if m16 == "1" and Cst == 32 else 1)
+            assert info["fused"] == 1
             Cc, KT, n_conv = info["C"], info["KT"], info["n_conv"]
             assert Cc == Cst and KT == cfg.resblock_kernel_sizes[j]
             dils = cfg.resblock_dilation_sizes[j]
@@ -365,14 +363,9 @@ def test_resblock_stream_packing_and_windowing(pkg, preset, m16, monkeypatch):
             if Cc == 64:  # narrow 256-column window (2 blocks per CU) only for k = 3
                 assert nwin == (256 if KT == 3 else 512)
             lane = np.arange(64)
-            if info["fused"] == 2:
-                # resblock16: [wave_m][conv][g32][tap][row tile][plane][lane][8]
-                u = packed.view(np.uint16).reshape(Cc // 32, n_conv, Cc // 32, KT, 2, 2, 64, 8)
-                val = bf2f(u[..., 0, :, :]).astype(np.float64) + bf2f(u[..., 1, :, :])
-            else:
-                # resblock: [wave_m][conv][g][tap][plane][lane][8]
-                u = packed.view(np.uint16).reshape(Cc // 32, n_conv, Cc // 16, KT, 2, 64, 8)
-                val = bf2f(u[:, :, :, :, 0]).astype(np.float64) + bf2f(u[:, :, :, :, 1])
+            # resblock: [wave_m][conv][g][tap][plane][lane][8]
+            u = packed.view(np.uint16).reshape(Cc // 32, n_conv, Cc // 16, KT, 2, 64, 8)
+            val = bf2f(u[:, :, :, :, 0]).astype(np.float64) + bf2f(u[:, :, :, :, 1])
             Ws = []
             for e in range(n_conv):
                 m, second = divmod(e, 2)
@@ -380,14 +373,6 @@ def test_resblock_stream_packing_and_windowing(pkg, preset, m16, monkeypatch):
                 W = sd[mod + ".weight"].astype(np.float64)
                 rec = np.zeros_like(W)
                 for wm in range(Cc // 32):
-                    if info["fused"] == 2:
-                        for ti in range(2):
-                            rows = wm * 32 + 16 * ti + (lane & 15)
-                            for g in range(Cc // 32):
-                                for el in range(8):
-                                    ci = g * 32 + 16 * (el >> 2) + 4 * (lane >> 4) + (el & 3)
-                                    rec[rows, ci, :] = val[wm, e, g, :, ti, lane, el]
-                        continue
                     rows = wm * 32 + (lane & 31)
                     for g in range(Cc // 16):
                         for el in range(8):

@@ -95,11 +95,11 @@ def test_golden_fixture_bf16x3(pkg, golden_index, name):
     assert rel < 1e-3, rel
 
 
-@pytest.mark.parametrize("big_tile,fused,wn32,m16",
-                         [("3", "1", "4", "1"), ("3", "0", "8", "0"), ("3", "1", "8", "0"),
-                          ("0", "1", "8", "1"), ("0", "0", "4", "1")])
+@pytest.mark.parametrize("big_tile,fused,wn32",
+                         [("3", "1", "4"), ("3", "0", "8"), ("3", "1", "8"), ("0", "1", "8"),
+                          ("0", "0", "4")])
 @pytest.mark.parametrize("preset,B,T", [("v1", 2, 300), ("v2star", 2, 200)])
-def test_bf16x3_vs_oracle_longer(pkg, preset, B, T, big_tile, fused, wn32, m16, monkeypatch):
+def test_bf16x3_vs_oracle_longer(pkg, preset, B, T, big_tile, fused, wn32, monkeypatch):
     """Random weights/mel vs the oracle, with each tile choice for the M >= 128 layers
     (HFG_BF16X3_BIGTILE: 0 = 128x256 8-wave, 3 = 128x256 4-wave with layer convs on tile 5
     — the default) and with the
@@ -109,7 +109,6 @@ def test_bf16x3_vs_oracle_longer(pkg, preset, B, T, big_tile, fused, wn32, m16, 
     monkeypatch.setenv("HFG_BF16X3_BIGTILE", big_tile)
     monkeypatch.setenv("HFG_FUSED_RB", fused)
     monkeypatch.setenv("HFG_RB_WN32", wn32)
-    monkeypatch.setenv("HFG_MFMA16", m16)
     dev = _dev()
     cfg = C.PRESETS[preset]
     sd = C.make_state_dict(cfg, seed=7)
@@ -117,13 +116,13 @@ def test_bf16x3_vs_oracle_longer(pkg, preset, B, T, big_tile, fused, wn32, m16, 
     wav = _run(_gen(pkg, cfg, sd, dev, precision="bf16x3"), mel, dev)
     ref = _oracle(cfg, sd, mel)
     err = np.abs(wav - ref).max()
-    print(f"{preset} B={B} T={T} [bf16x3 tile={big_tile} fused={fused} m16={m16}]: "
+    print(f"{preset} B={B} T={T} [bf16x3 tile={big_tile} fused={fused} wn32={wn32}]: "
           f"max err {err:.3e}")
     assert err < ATOL
 
 
-@pytest.mark.parametrize("wn32,m16", [("4", "1"), ("8", "1"), ("4", "0")])
-def test_fused_resblock_matches_layer_path(pkg, wn32, m16, monkeypatch):
+@pytest.mark.parametrize("wn32", ["4", "8"])
+def test_fused_resblock_matches_layer_path(pkg, wn32, monkeypatch):
     """Whole-ResBlock kernel vs the layer-per-launch bf16x3 schedule on a ragged batch
     long enough for many windows per utterance (window seams, lengths that end inside
     a window, an utterance shorter than one window)."""
@@ -138,7 +137,6 @@ def test_fused_resblock_matches_layer_path(pkg, wn32, m16, monkeypatch):
     for fused in ("0", "1"):
         monkeypatch.setenv("HFG_FUSED_RB", fused)
         monkeypatch.setenv("HFG_RB_WN32", wn32)
-        monkeypatch.setenv("HFG_MFMA16", m16)
         gen = _gen(pkg, cfg, sd, dev, precision="bf16x3")
         with torch.no_grad():
             outs.append(gen(mel, lengths=lens).cpu().numpy())

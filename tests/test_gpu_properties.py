@@ -256,12 +256,12 @@ def test_full_size_bf16x3_batch_split_invariance(full_bf16x3, dev):
 
 
 # ---- maximum size ------------------------------------------------------------------
-T_MAX = 131072  # V1: 8192 * T fp32 per item = 2^30 elements, the kernels' 32-bit byte offsets
+T_MAX = 131071  # V1: 8192 * T fp32 per item < 2^30 elements, the kernels' 32-bit byte offsets
 
 
 @pytest.mark.parametrize("precision", ["bf16x3", "fp32"])
 def test_max_length_utterance_windowed_oracle(pkg, dev, precision):
-    """One utterance at the longest T the C ABI accepts (2^30 activation elements per
+    """One utterance at the longest T the C ABI accepts (2^30 - 8192 activation elements per
     item, ~25 min of audio): the output at the head, the middle and the very end matches
     the oracle on a receptive-field window, so no byte offset wraps."""
     from oracle import config as C, hifigan_torch as H
@@ -297,7 +297,7 @@ def test_over_max_length_rejected(pkg, v1, dev):
                             ctypes.c_void_p(dummy.data_ptr()), L, ctypes.c_void_p(dummy.data_ptr()),
                             256, None)
     assert rc == -22
-    assert b"exceeds 2^30" in lib.hfg_last_error()
+    assert b"reaches 2^30" in lib.hfg_last_error()
 
 
 # ---- weight tracking and 2-stream capture -------------------------------------------

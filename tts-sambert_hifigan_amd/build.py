@@ -14,7 +14,7 @@ PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(PKG_DIR, "csrc")
 LIB_NAME = "libhifigan_hip.so"
 LIB_PATH = os.path.join(PKG_DIR, LIB_NAME)
-SOURCES = ["conv_kernels.hip", "conv_bf16x3.hip", "resblock_bf16x3.hip", "resblock16_bf16x3.hip",
+SOURCES = ["conv_kernels.hip", "conv_bf16x3.hip", "resblock_bf16x3.hip",
            "mrf_thin.hip", "mrf_thin_mfma.hip", "ups_bf16x3.hip", "probe.hip", "hifigan_capi.cpp",
            "mel_kernels.hip",
            "mel_capi.cpp"]

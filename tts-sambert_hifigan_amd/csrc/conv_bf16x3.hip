@@ -178,8 +178,9 @@ conv1d_bf16x3(const ConvParams p) {
     if (x_short) wait_vm<(N >= 8 ? N - 8 : 0)>();
     else wait_vm<N>();
   };
-  // whole 32-bit range: an item holds up to 2^30 floats (4 GiB), and every offset the
-  // staging forms stays below that (byte offsets are unsigned 32-bit, as before)
+  // whole 32-bit range: an item holds fewer than 2^30 floats (the C ABI refuses 2^30:
+  // the hardware drops a dword whose end passes num_records 0xFFFFFFFF, which would be
+  // a 4-GiB item's last float), and every offset the staging forms stays below that
   const __amdgpu_buffer_rsrc_t xrs =
       __builtin_amdgcn_make_buffer_rsrc((void*)xb, 0, -1, 0x00020000);
   // whole 16-channel groups (every group of the V1 / V2* layers): the window mask and the

@@ -322,7 +322,7 @@ conv_post4_tanh(const float* __restrict__ x, int64_t x_bs, int C, int L, const f
     *reinterpret_cast<f4*>(out) = f4{0.f, 0.f, 0.f, 0.f};
     return;
   }
-  // an item holds at most 2^30 floats: byte offsets from the item base fit 32 bits (a
+  // an item holds fewer than 2^30 floats: byte offsets from the item base fit 32 bits (a
   // buffer descriptor cannot: a 4-GiB item's range does not fit its 32-bit record count)
   const char* xb = reinterpret_cast<const char*>(x + (int64_t)b * x_bs);
   // the three quads [t-4, t), [t, t+4), [t+4, t+8); element k of v = x[t - 4 + k]

@@ -108,7 +108,6 @@ struct ProfRec {
 struct RbFused {
   std::vector<int> convs;     // layer indices in execution order conv1_0, conv2_0, conv1_1, ...
   bool fused = false;         // this ResBlock runs as one resblock_bf16x3 launch
-  bool m16 = false;           // ... on the 16x16x32 MFMA shape (resblock16_bf16x3)
   int kt = 0, halo = 0, W = 0, waves_n = 0;
   // split into two launches (convs [0, split) then [split, n)): each part's window pays
   // only its own receptive-field halo; the first writes x to scratch (0: one launch)
@@ -169,7 +168,6 @@ struct hfg_handle {
   double rb_split_min = 0.9; // split when its MFMA work <= this x one launch's (HFG_RB_SPLIT_MIN)
   int rb_waves_n32 = 4;      // window of the C = 32 ResBlock kernel: 128 * this columns
                              // (HFG_RB_WN32: 4 or 8)
-  bool mfma16 = true;        // 16x16x32-shape ResBlock kernel for C = 32 (HFG_MFMA16=0: off)
   int ups_swizzle = 1;       // XCD swizzle of the upsampler blocks (HFG_UPS_SWIZZLE=0: off)
   bool post4 = true;         // conv_post on the 4-samples-per-thread kernel where L % 4 == 0
                              // (HFG_POST4=0: the LDS-staged kernel; bitwise the same wav)
@@ -454,8 +452,6 @@ int build_layers(hfg_handle* h) {
       if (C == 128 && (double)nwin / rb.W > 1.15) ok = false;
       if (!ok) continue;
       rb.fused = true;
-      // 16x16x32 shape: measured 3-4% faster for C = 32, 2-10% slower for C >= 64 (r01)
-      rb.m16 = h->mfma16 && C == 32 && hfg::rb16_supported(C, rb.kt, waves_n);
       // two launches where that cuts the MFMA work (windows / W, weighted by the convs of
       // each part) by >= 10 %: the extra x write + read costs less than that at C <= 64
       if (h->rb_split && C <= 64 && c.n_dil[j] >= 2) {
@@ -685,9 +681,6 @@ void pack_bf16x3(const Layer& L, F wt, uint16_t* dst) {
 //   row = wave_m*32 + (lane & 31), ci = g*16 + 4*(lane >> 5) + (el & 3) + 8*(el >> 2)
 // (the permuted channel order of the kernel's operand planes); plane 0 = bf16(w),
 // plane 1 = bf16(w - hi).  Biases [conv][C].
-// A stream of resblock16_bf16x3 (16x16x32 shape):
-//   idx = ((((((wave_m*n_conv + e)*(C/32) + g)*KT + tap)*2 + i)*2 + plane)*64 + lane)*8 + el
-//   row = wave_m*32 + 16*i + (lane & 15), ci = g*32 + 16*(el >> 2) + 4*(lane >> 4) + (el & 3)
 void pack_resblock(hfg_handle* h, const RbFused& rb) {
   uint16_t* dst = reinterpret_cast<uint16_t*>(h->packed_host.data() + rb.w_off);
   float* bdst = h->packed_host.data() + rb.b_off;
@@ -695,24 +688,7 @@ void pack_resblock(hfg_handle* h, const RbFused& rb) {
   const int C = h->layers[rb.convs[0]].C_out;
   const int KT = rb.kt, n_g = C / 16;
   size_t idx = 0;
-  for (int wm = 0; wm < C / 32 && rb.m16; ++wm)
-    for (int e = 0; e < n_conv; ++e) {
-      const Layer& L = h->layers[rb.convs[e]];
-      const float* w = h->params[L.mod + ".weight"].data.data();  // [C_out][C_in][k]
-      for (int g = 0; g < C / 32; ++g)
-        for (int tap = 0; tap < KT; ++tap)
-          for (int i = 0; i < 2; ++i)
-            for (int plane = 0; plane < 2; ++plane)
-              for (int lane = 0; lane < 64; ++lane)
-                for (int el = 0; el < 8; ++el) {
-                  const int row = wm * 32 + 16 * i + (lane & 15);
-                  const int ci = g * 32 + 16 * (el >> 2) + 4 * (lane >> 4) + (el & 3);
-                  const float v = w[((size_t)row * C + ci) * KT + tap];
-                  const uint16_t hi = f2bf(v);
-                  dst[idx++] = plane == 0 ? hi : f2bf(v - bf2f(hi));
-                }
-    }
-  for (int wm = 0; wm < C / 32 && !rb.m16; ++wm)
+  for (int wm = 0; wm < C / 32; ++wm)
     for (int e = 0; e < n_conv; ++e) {
       const Layer& L = h->layers[rb.convs[e]];
       const float* w = h->params[L.mod + ".weight"].data.data();  // [C_out][C_in][k]
@@ -1104,8 +1080,7 @@ int run_resblock(hfg_handle* h, Launcher& ln, const RbFused& rb, const float* x,
     const char* name = nullptr;
     ln.begin(flop, bytes);
     hipError_t e =
-        rb.m16 ? hfg::launch_resblock16_bf16x3(C, rb.waves_n, rb.kt, h->np, p, (int)B, ln.stream, &name)
-               : hfg::launch_resblock_bf16x3(C, rb.waves_n, rb.kt, h->np, p, (int)B, ln.stream, &name);
+        hfg::launch_resblock_bf16x3(C, rb.waves_n, rb.kt, h->np, p, (int)B, ln.stream, &name);
     ln.end(name);
     if (e != hipSuccess)
       return fail(HFG_EIO, "launch resblock %s: %s", L0.mod.c_str(), hipGetErrorString(e));
@@ -1380,9 +1355,11 @@ int forward_impl(hfg_handle* h, const float* mel, int64_t B, int64_t T, const hf
     return fail(HFG_EINVAL, "out_len %lld != expected %lld", (long long)out_len,
                 (long long)sh.L.back());
   // the kernels address one utterance's activations with 32-bit byte offsets from a
-  // per-item base: at most 2^30 fp32 elements per item (V1: T <= 131072 frames)
-  if (sh.item_elems > ((int64_t)1 << 30))
-    return fail(HFG_EINVAL, "per-item activation of %lld elements exceeds 2^30 (T too long)",
+  // per-item base, through buffer descriptors of num_records 0xFFFFFFFF.  The hardware
+  // drops a dword whose END passes num_records, so a 4 GiB item would lose its last
+  // float: an item holds fewer than 2^30 fp32 elements (V1: T <= 131071 frames)
+  if (sh.item_elems >= ((int64_t)1 << 30))
+    return fail(HFG_EINVAL, "per-item activation of %lld elements reaches 2^30 (T too long)",
                 (long long)sh.item_elems);
   if (ws_len < ws_part_bytes(h, B, T, conc_ok)) return fail(HFG_EINVAL, "workspace too small");
   const int nb = n_bufs(h, B, T, conc_ok);
@@ -1519,7 +1496,6 @@ int create_impl(const hfg_config* cfg, bool mrf_only, int device, hfg_handle** o
     if (v == 0 || v == 3) h->big_tile = v;
   }
   if (const char* fe = getenv("HFG_FUSED_RB")) h->use_fused_rb = atoi(fe) != 0;
-  if (const char* me = getenv("HFG_MFMA16")) h->mfma16 = atoi(me) != 0;
   if (const char* te = getenv("HFG_THIN")) h->thin = atoi(te) != 0;
   if (const char* tm = getenv("HFG_THIN_MFMA")) h->thin_mfma = atoi(tm);
   if (const char* st = getenv("HFG_SMALL_TILE")) h->small_tile = atoi(st);
@@ -1791,8 +1767,8 @@ int mrf_check(hfg_handle* h, const float* x, int64_t B, int64_t L, float* y, voi
   if (!x || !y || !ws) return fail(HFG_EINVAL, "x / y / workspace pointer is NULL");
   if (x == y) return fail(HFG_EINVAL, "y must not alias x");
   if (B <= 0 || L <= 0) return fail(HFG_EINVAL, "B and L must be > 0");
-  if ((int64_t)h->stages[0].C * L > ((int64_t)1 << 30))
-    return fail(HFG_EINVAL, "per-item activation exceeds 2^30 elements");
+  if ((int64_t)h->stages[0].C * L >= ((int64_t)1 << 30))
+    return fail(HFG_EINVAL, "per-item activation reaches 2^30 elements");
   return HFG_OK;
 }
 size_t mrf_ws_bytes(const hfg_handle* h, int64_t B, int64_t L) {
@@ -1992,7 +1968,7 @@ int hfg_debug_packed_resblock(hfg_handle* h, int stage, int j, float* out, size_
   if (j < 0 || j >= (int)st.rbs.size()) return fail(HFG_EINVAL, "resblock out of range");
   const RbFused& rb = st.rbs[j];
   if (!rb.fused) return HFG_OK;
-  info[0] = rb.m16 ? 2 : 1;  // 1: resblock_bf16x3 stream order, 2: resblock16_bf16x3
+  info[0] = 1;  // fused (resblock_bf16x3 stream order)
   info[1] = h->layers[rb.convs[0]].C_out;
   info[2] = rb.kt;
   info[3] = (int64_t)rb.convs.size();

@@ -232,11 +232,6 @@ bool rb_supported(int C, int kt, int waves_n);
 size_t rb_lds_bytes(int C, int waves_n, int n_conv);
 hipError_t launch_resblock_bf16x3(int C, int waves_n, int kt, int np, const RbParams& p,
                                   int batch, hipStream_t stream, const char** name);
-// the same on the 16x16x32 MFMA shape (resblock16_bf16x3.hip); A stream packed
-// [wave_m][conv][group32][tap][row tile][plane][lane][8]
-bool rb16_supported(int C, int kt, int waves_n);
-hipError_t launch_resblock16_bf16x3(int C, int waves_n, int kt, int np, const RbParams& p,
-                                    int batch, hipStream_t stream, const char** name);
 
 // ---- whole MRF per launch for thin stages, C <= 16 (mrf_thin.hip) ----
 // All ResBlocks of one MRF on a time window in LDS, packed-fp32 VALU dot products (exact

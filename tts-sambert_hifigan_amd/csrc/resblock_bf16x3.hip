@@ -113,8 +113,10 @@ resblock_bf16x3(const RbParams p) {
   // ---- x and the MRF accumulator of utterance b through buffer descriptors ----
   // Element (row, column) sits at soffset = (row0 + row part of accumulator element r) * L * 4
   // (wave-uniform: SALU) + voffset = (4 * half * L + column) * 4 (one VGPR per column tile):
-  // no per-element address VALU and no branches.  An item is at most 2^30 floats, so every
-  // offset fits 32 bits; the range is never relied on (masked lanes read offset 0).
+  // no per-element address VALU and no branches.  An item is fewer than 2^30 floats (the C
+  // ABI's bound: a dword is dropped when voffset + soffset + 4 passes num_records, so a
+  // 4-GiB item would lose its last float), so every offset and its dword end fit 32 bits;
+  // the range is never relied on otherwise (masked lanes read offset 0).
   const unsigned Lb = (unsigned)p.L * 4u;
   auto srow = [&](int r) { return (unsigned)(row0 + (r & 3) + 8 * (r >> 2)) * Lb; };
   const unsigned lrow = 4u * (unsigned)half * (unsigned)p.L;

@@ -9,7 +9,8 @@
 // tail tile of one column), and every class has one block-uniform input offset per tap.
 // GEMM rows of a class: rr = co*h + s' (s' = s - class*h); a wave computes BOTH classes of
 // its rows and columns, so a lane ends up holding whole runs of consecutive samples:
-//   u = 2 (h = 1): (L, R) = samples 2m, 2m+1 of one channel        -> one 8-B store
+//   u = 2 (h = 1): (L, R) = samples 2m, 2m+1 of one channel; a DPP swap with the lane of
+//                  frame m^1 makes it 4 samples -> one 16-B store per channel pair
 //   u = 4 (h = 2): rows (co,0),(co,1) x (L, R) = samples 4m..4m+3 -> one 16-B store
 //   h % 4 == 0:    4 consecutive rows = 4 consecutive samples      -> 16-B stores per class
 // (the polyphase kernel in conv_bf16x3.hip stores u = 2 stages one dword per value).
