@@ -43,6 +43,10 @@
 #define HFG_UPS_PAIR 1
 #endif
 
+#ifndef HFG_UPS_SMALL_OCC
+#define HFG_UPS_SMALL_OCC 3
+#endif
+
 namespace hfg {
 
 namespace {
@@ -50,8 +54,13 @@ typedef float floatx2 __attribute__((ext_vector_type(2)));
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 }  // namespace
 
+// occupancy: the small tile (2 x 32 x 32 accumulators per class) fits 168 VGPRs, 3 waves per
+// SIMD; its launches (the thin last upsampler) are bound by HBM latency, not the matrix pipe
+template <int WAVES_M, int WAVES_N, int WM, int WN>
+constexpr int ups_min_blocks() { return WAVES_M * WM * WN <= 2 ? HFG_UPS_SMALL_OCC : 2; }
+
 template <int WAVES_M, int WAVES_N, int WM, int WN, int NP>
-__global__ void __launch_bounds__(64 * WAVES_M * WAVES_N, 2)
+__global__ void __launch_bounds__(64 * WAVES_M * WAVES_N, (ups_min_blocks<WAVES_M, WAVES_N, WM, WN>()))
 ups_bf16x3(const UpsParams p) {
   constexpr int NW = WAVES_M * WAVES_N;
   constexpr int MT = 32 * WM * WAVES_M;      // rows per class and m-tile
