@@ -169,6 +169,8 @@ struct hfg_handle {
   int rb_waves_n32 = 4;      // window of the C = 32 ResBlock kernel: 128 * this columns
                              // (HFG_RB_WN32: 4 or 8)
   int ups_swizzle = 1;       // XCD swizzle of the upsampler blocks (HFG_UPS_SWIZZLE=0: off)
+  int ups_small_rows = 0;    // output-frame upsamplers of at most this many rows per class on
+                             // the 32-row tile (HFG_UPS_SMALL_ROWS)
   bool post4 = true;         // conv_post on the 4-samples-per-thread kernel where L % 4 == 0
                              // (HFG_POST4=0: the LDS-staged kernel; bitwise the same wav)
   int ups_frames = 1;        // k = 2u upsamplers on the output-frame kernel: 1 when its grid
@@ -384,8 +386,12 @@ int build_layers(hfg_handle* h) {
       const int rows_f = L.kind == L_UPS ? L.C_out * L.s / 2 : 0;
       if (L.kind == L_UPS && h->ups_frames && L.k == 2 * L.s && hfg::ups_rate_ok(L.s) &&
           L.p == L.s / 2 && L.C_in % 16 == 0) {
-        const int cfg = rows_f % hfg::kUpsCfgs[0].MT() == 0   ? 0
-                        : rows_f % hfg::kUpsCfgs[1].MT() == 0 ? 1
+        // the 32-row tile (3 waves per SIMD) where the 64-row one does not divide the rows,
+        // or up to HFG_UPS_SMALL_ROWS rows
+        const bool small = rows_f % hfg::kUpsCfgs[1].MT() == 0 &&
+                           (rows_f % hfg::kUpsCfgs[0].MT() != 0 || rows_f <= h->ups_small_rows);
+        const int cfg = small                                 ? 1
+                        : rows_f % hfg::kUpsCfgs[0].MT() == 0 ? 0
                                                                : -1;
         if (cfg >= 0) {
           const hfg::UpsCfg& tf = hfg::kUpsCfgs[cfg];
@@ -1501,6 +1507,7 @@ int create_impl(const hfg_config* cfg, bool mrf_only, int device, hfg_handle** o
   if (const char* st = getenv("HFG_SMALL_TILE")) h->small_tile = atoi(st);
   if (const char* rc = getenv("HFG_RB_CONC")) h->rb_conc = atoi(rc);
   if (const char* us = getenv("HFG_UPS_SWIZZLE")) h->ups_swizzle = atoi(us);
+  if (const char* us = getenv("HFG_UPS_SMALL_ROWS")) h->ups_small_rows = atoi(us);
   if (const char* uf = getenv("HFG_UPS_FRAMES")) h->ups_frames = atoi(uf);
   if (const char* pq = getenv("HFG_POST4")) h->post4 = atoi(pq) != 0;
   if (const char* el = getenv("HFG_EPI_LDS")) h->epi_lds = atoi(el);
