@@ -35,6 +35,10 @@
  *     passed as void*; NULL = default stream): no host synchronisation and no
  *     allocation when weights are committed and the workspace is large enough,
  *     so it may be captured into a hipGraph.
+ *   - Size limit: the kernels address one utterance with 32-bit byte offsets, so
+ *     its largest stage activation (C x L) must hold fewer than 2^30 floats
+ *     (V1: T <= 131071 frames, ~25 min of 22.05 kHz audio); a longer T is
+ *     refused with HFG_EINVAL before any launch.
  *   - One handle per device.  Calls on one handle are serialised by a
  *     per-handle lock (a forward enqueues its launches, then releases it);
  *     hfg_forward with the internal workspace must not be used from two
@@ -68,8 +72,8 @@ extern "C" {
  *            exact fp32 products (the parity reference mode), every other conv.
  *   BF16X3 : every fp32 operand split as hi = bf16(v), lo = bf16(v - hi);
  *            hi*hi + hi*lo + lo*hi accumulated in fp32 on the bf16 matrix cores
- *            (~16-bit-mantissa products, 5.3x the fp32 MFMA rate): conv_pre, every
- *            upsampler whose polyphase GEMM has >= 32 rows (all four in V1), the
+ *            (~16-bit-mantissa products, 5.3x the fp32 MFMA rate): conv_pre, the
+ *            upsamplers (k = 2u: an output-frame GEMM; else polyphase, >= 32 rows), the
  *            whole-ResBlock kernels of the C = 32/64/128 stages and the layer convs
  *            of C >= 32; convs whose (k-1)*dilation exceeds the bf16x3 window fall
  *            back to the fp32 kernels.  Output within ~1e-5 of the reference at
