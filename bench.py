@@ -60,22 +60,38 @@ PEAK_HBM_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 PEAK_BF16_TFLOPS = 2500.0  # MI355X_MICROARCH.md: BF16 MFMA dense (no sparsity)
 
 
+# position of the NP (MFMA products per multiply-add) and FMT (split format) template
+# arguments of the split-precision kernels, as hfg_profile_summary / rocprofv3 print them
+_SPLIT_ARGS = {"conv1d_bf16x3": (8, 10), "ups_bf16x3": (4, 5), "resblock_bf16x3": (3, 4),
+               "mrf_thin_mfma": (1, 2)}
+
+
+def kernel_split(name: str):
+    """(MFMA products per algorithmic multiply-add, split format "f16" / "bf16") of a
+    split-precision kernel; (0, None) for the fp32-MFMA / VALU kernels."""
+    base = name.split("<")[0].split("(")[0].strip()
+    if base not in _SPLIT_ARGS or "<" not in name:
+        return 0, None
+    args = [a.strip() for a in name.split("<", 1)[1].split(">")[0].split(",")]
+    i_np, i_fmt = _SPLIT_ARGS[base]
+    np_ = int(args[i_np]) if len(args) > i_np else 3
+    fmt = "f16" if len(args) > i_fmt and args[i_fmt] == "1" else "bf16"
+    return np_, fmt
+
+
 def kernel_products(name: str) -> int:
-    """bf16 MFMA products per algorithmic multiply-add of a kernel (0: fp32 MFMA)."""
-    if "bf16x3" in name or "mrf_thin_mfma" in name:
-        # conv1d_bf16x3, resblock[16]_bf16x3, conv_ws_bf16x3, mrf_thin_mfma: 3 bf16 MFMA
-        # products (hi*hi + hi*lo + lo*hi) per algorithmic multiply-add, 2 for the bf16w
-        # instances (last template argument NP = 2: lo(w) = 0 skipped)
-        return 2 if name.replace(" ", "").split("(")[0].endswith(",2>") else 3
-    return 0
+    """MFMA products per algorithmic multiply-add of a kernel (0: fp32 MFMA / VALU): 3 for
+    the split kernels (hi*hi + hi*lo + lo*hi, f16 or bf16 halves), 2 for the bf16w instances
+    (NP = 2: lo(w) = 0 skipped)."""
+    return kernel_split(name)[0]
 
 
 def kernel_peak(name: str):
     """(peak in algorithmic fp32-conv TFLOP/s, description) for one kernel."""
-    np_ = kernel_products(name)
+    np_, fmt = kernel_split(name)
     if np_:
         return (PEAK_BF16_TFLOPS / np_,
-                f"bf16 dense MFMA 2.5 PFLOP/s / {np_} split products")
+                f"{fmt} dense MFMA 2.5 PFLOP/s / {np_} split products")
     return PEAK_FP32_TFLOPS, "fp32 MFMA 157.3 TFLOP/s"
 
 
@@ -102,7 +118,7 @@ def parse():
     ap.add_argument("--preset", default="v1", choices=["v1", "v2star"])
     ap.add_argument("--batch", type=int, default=8, help="utterances per GPU")
     ap.add_argument("--frames", type=int, default=1024)
-    ap.add_argument("--precision", default="bf16x3", choices=["fp32", "bf16x3", "bf16w"],
+    ap.add_argument("--precision", default="bf16x3", choices=["fp32", "f16x3", "bf16x3", "bf16w"],
                     help="conv arithmetic: bf16x3 split-precision MFMA (default; parity 1e-4 "
                          "met, tests/test_gpu_parity.py), exact fp32 MFMA, or bf16w (weights "
                          "stored as bf16: a different model, parity against the bf16-rounded "
@@ -628,10 +644,7 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f32" if args.precision == "fp32" else args.precision,
-        "dtype_note": ("fp32 operands on the fp32 MFMA (exact products)" if args.precision == "fp32"
-                       else "fp32 in/out and fp32 accumulation; every fp32 operand split into bf16 "
-                            "hi + lo, products hi*hi + hi*lo + lo*hi on the bf16 MFMA (the "
-                            "upsamplers too). " + PREC.note(args.precision)),
+        "dtype_note": PREC.dtype_note(args.precision),
         "precision_limit": ({f"x{k:g}": v for k, v in PREC.BF16X3_SCALE_LIMITS.items()}
                             if args.precision == "bf16x3" else None),
         "precision_measured": PREC.MEASURED.get(args.precision),
@@ -733,13 +746,13 @@ def main():
         all_flop = sum(v["flop"] for v in prof.values()) / args.steps
         all_bytes = sum(v["bytes"] for v in prof.values()) / args.steps
         step_s = elapsed / args.steps
-        issue = {"bf16x3": 3.0, "bf16w": 2.0}.get(args.precision, 1.0)
+        issue = {"f16x3": 3.0, "bf16x3": 3.0, "bf16w": 2.0}.get(args.precision, 1.0)
         line["roofline_step"] = {
             "compute_TFLOPs": all_flop / step_s / 1e12,
             "mfma_issue_frac": (all_flop * issue / step_s / 1e12 /
                                 (PEAK_BF16_TFLOPS if args.precision != "fp32" else PEAK_FP32_TFLOPS)),
-            "mfma_issue_note": (f"algorithmic FLOP x {issue:.0f} bf16 MFMA products per multiply-add "
-                                "/ step time / 2.5 PF bf16 dense peak" if args.precision != "fp32" else
+            "mfma_issue_note": (f"algorithmic FLOP x {issue:.0f} f16/bf16 MFMA products per "
+                                "multiply-add / step time / 2.5 PF dense peak" if args.precision != "fp32" else
                                 "algorithmic FLOP / step time / 157.3 TF fp32 MFMA peak"),
             "hbm_model_GBs": all_bytes / step_s / 1e9,
             "hbm_model_frac": all_bytes / step_s / 1e9 / PEAK_HBM_GBS,

@@ -65,28 +65,34 @@ extern "C" {
 #define HFG_EAGAIN (-11)   /* weights incomplete (a key was never set)    */
 #define HFG_EIO (-5)       /* HIP runtime error (launch, memcpy, ...)     */
 
-/* Arithmetic of the Generator's convolutions.  In both modes conv_post + tanh and
- * the MRFs of thin stages (C <= 16 channels, e.g. V2*'s last two: one mrf_thin launch
- * per MRF on the packed-fp32 vector ALUs) compute exact fp32 products.
- *   FP32   : fp32 operands on the fp32 matrix cores (v_mfma_f32_32x32x2_f32),
- *            exact fp32 products (the parity reference mode), every other conv.
- *   BF16X3 : every fp32 operand split as hi = bf16(v), lo = bf16(v - hi);
- *            hi*hi + hi*lo + lo*hi accumulated in fp32 on the bf16 matrix cores
- *            (~16-bit-mantissa products, 5.3x the fp32 MFMA rate): conv_pre, the
- *            upsamplers (k = 2u: an output-frame GEMM; else polyphase, >= 32 rows), the
- *            whole-ResBlock kernels of the C = 32/64/128 stages and the layer convs
- *            of C >= 32; convs whose (k-1)*dilation exceeds the bf16x3 window fall
- *            back to the fp32 kernels.  Output within ~1e-5 of the reference at
- *            default weight scale (1e-4 bar; DESIGN.md §4 gives the x4-scale limit).
- *   BF16W  : bf16 weight storage — every conv weight rounded to bf16 (nearest-even)
- *            when the weights are committed, activations still split hi/lo: hi*hi +
- *            hi*lo on the bf16 matrix cores (2 MFMAs per multiply-add instead of 3),
- *            exact products of the bf16-rounded weights elsewhere.  Output is that of
- *            the reference Generator whose weights were cast to bf16 (1e-4 bar against
- *            that model), not of the fp32-weight model.  Biases stay fp32. */
+/* Arithmetic of the Generator's convolutions.  In every mode conv_post + tanh and the MRF
+ * of a C = 8 stage (V2*'s last: one mrf_thin launch on the packed-fp32 vector ALUs) compute
+ * exact fp32 products.
+ *   FP32   : fp32 operands on the fp32 matrix cores (v_mfma_f32_32x32x2_f32), exact fp32
+ *            products, every other conv.  157 TFLOP/s peak.
+ *   F16X3  : (the default of the Python module) every fp32 operand scaled by a power of two
+ *            and split into f16 halves hi = f16(v 2^e), lo = f16(v 2^e - hi) (22 significant
+ *            bits); hi*hi + hi*lo + lo*hi accumulated in fp32 on the f16 matrix cores
+ *            (v_mfma_f32_32x32x16_f16 / 16x16x32, 5.3x the fp32 MFMA rate).  Activation
+ *            scales are per (tensor, batch item), from the producing kernel's max |value|,
+ *            or per block inside a whole-ResBlock / whole-MRF kernel; weight scales per
+ *            layer.  Products within ~2^-21 relative of exact: fp32-class output (within
+ *            the reference's own fp32 rounding on every golden fixture, x4 weights included).
+ *            Used by conv_pre, the upsamplers, the whole-ResBlock kernels of the C = 32 / 64
+ *            / 128 stages, the C = 16 thin MRF and the layer convs of C >= 32; convs whose
+ *            (k-1)*dilation exceeds the split kernels' window fall back to the fp32 kernels.
+ *   BF16X3 : the same kernels with bf16 halves, unscaled: ~16-bit-mantissa products (within
+ *            ~1e-5 of the reference at default weight scale; DESIGN.md §4 gives its x4 limit).
+ *   BF16W  : bf16 weight storage — every conv weight rounded to bf16 (nearest-even) when
+ *            the weights are committed; on the F16X3 kernels with the activations still split:
+ *            hi(w)*hi(x) + hi(w)*lo(x) (2 MFMAs per multiply-add instead of 3), exact products
+ *            of the bf16-rounded weights elsewhere.  Output is that of the reference
+ *            Generator whose weights were cast to bf16 (1e-4 bar against that model), not of
+ *            the fp32-weight model.  Biases stay fp32. */
 #define HFG_DTYPE_FP32 0
 #define HFG_DTYPE_BF16X3 1
 #define HFG_DTYPE_BF16W 2
+#define HFG_DTYPE_F16X3 3
 
 typedef struct hfg_handle hfg_handle;
 

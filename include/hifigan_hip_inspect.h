@@ -19,15 +19,17 @@ extern "C" {
 #endif
 
 /* Copy the packed image of one layer (module prefix, e.g. "ups.0") into out:
- * w_len packed GEMM weights followed by b_len per-row biases.  info[10]
+ * w_len packed GEMM weights followed by b_len per-row biases.  info[11]
  * receives {kind (0 conv, 1 ups, 2 post), M, KT, tile, m_tiles, n_chunks,
- * w_len, b_len, CK, MT}.  With out == NULL only info is filled. */
+ * w_len, b_len, CK, MT, ew} (ew: the f16x3 packing exponent — the split planes hold
+ * f16 halves of w * 2^ew; 0 otherwise).  With out == NULL only info is filled. */
 int hfg_debug_packed_layer(hfg_handle* h, const char* mod, float* out, size_t cap,
                            int64_t* info);
 
 /* Packed image of the whole-ResBlock launch of stage `stage`, ResBlock `j`
- * (resblock_bf16x3.hip; bf16x3 handles, stages with 32 or 64 channels):
- * w_len floats of A stream (bf16 hi/lo pairs) followed by b_len biases.
+ * (resblock_bf16x3.hip; split-precision handles, stages with 32, 64 or 128 channels):
+ * w_len floats of A stream (hi/lo pairs of each conv's split format and exponent, as
+ * hfg_debug_packed_layer of that conv reports) followed by b_len biases.
  * info[8] receives {fused (0/1), C, KT, n_conv, halo, W, w_len, b_len}.
  * Returns HFG_OK with info[0] = 0 when the stage runs layer by layer. */
 int hfg_debug_packed_resblock(hfg_handle* h, int stage, int j, float* out, size_t cap,
@@ -48,7 +50,9 @@ int hfg_forward_taps(hfg_handle* h, const float* mel, int64_t B, int64_t T, floa
  * launch of iters / 4).  kind 0: v_mfma_f32_32x32x16_bf16, kind 1:
  * v_mfma_f32_32x32x2_f32, 4 independent accumulator chains per wave; kinds 2 / 3: the
  * same with one chain (each MFMA accumulates onto the previous one's result; 8 MFMAs
- * per round instead of 32).  *tflops <- dense TFLOP/s over the timed launch (HIP events),
+ * per round instead of 32); kinds 4 / 5: v_mfma_f32_32x32x16_f16 (the f16x3 kernels'
+ * instruction) on operands with random 10-bit mantissas, 4 chains / 1 chain.
+ * *tflops <- dense TFLOP/s over the timed launch (HIP events),
  * *mhz <- shader clock over it (s_memtime against the 100 MHz real-time counter).
  * Measurement only (bench.py's roofline "peak_sustained"); synchronous. */
 int hfg_probe_mfma_rate(int device, int kind, int iters, double* tflops, double* mhz);

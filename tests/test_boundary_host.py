@@ -127,10 +127,10 @@ def test_package_imports_by_underscore_name():
 
 
 def test_default_precision_from_environment(pkg, monkeypatch):
-    """Constructor default: exact fp32, or HFG_PRECISION (a reference code base switches its
-    Generator to the split-precision path without code changes); submodules follow."""
+    """Constructor default: f16x3 (fp32-class split products), or HFG_PRECISION (a reference
+    code base switches its Generator's arithmetic without code changes); submodules follow."""
     monkeypatch.delenv("HFG_PRECISION", raising=False)
-    assert pkg.HiFiGANGenerator(**C.V2STAR.kwargs()).precision == "fp32"
+    assert pkg.HiFiGANGenerator(**C.V2STAR.kwargs()).precision == "f16x3"
     monkeypatch.setenv("HFG_PRECISION", "bf16x3")
     gen = pkg.HiFiGANGenerator(**C.V2STAR.kwargs())
     assert gen.precision == "bf16x3"

@@ -206,16 +206,32 @@ def bf2f(u16):
     return (u16.astype(np.uint32) << 16).view(np.float32)
 
 
-@pytest.mark.parametrize("big_tile", ["0", "3", "areg"])
+def h2f(u16):
+    return np.ascontiguousarray(u16).view(np.float16).astype(np.float32)
+
+
+def dec(u16, precision, ew=0):
+    """A split plane's 16-bit values as float64: bf16 (bf16x3), or f16 halves of w * 2^ew
+    (f16x3 / bf16w: csrc/bf16x3_common.h)."""
+    if precision == "bf16x3":
+        return bf2f(u16).astype(np.float64)
+    return h2f(u16).astype(np.float64) * 2.0 ** -ew
+
+
+# reconstruction bound of hi + lo relative to the layer's max |w|: bf16 halves ~2^-16, scaled
+# f16 halves ~2^-22 (csrc/bf16x3_common.h)
+SPLIT_TOL = {"bf16x3": 2.0 ** -15, "f16x3": 2.0 ** -21}
+
+
+@pytest.mark.parametrize("precision", ["bf16x3", "f16x3"])
 @pytest.mark.parametrize("preset", ["v1", "v2star"])
-def test_bf16x3_packing(pkg, preset, big_tile, monkeypatch):
-    """bf16x3 layers: the packed hi/lo planes reconstruct every weight to ~2^-16
-    relative, in the fragment order of conv_bf16x3.hip (every tile for M >= 128)."""
-    monkeypatch.setenv("HFG_AREG", "1" if big_tile == "areg" else "0")
-    monkeypatch.setenv("HFG_BF16X3_BIGTILE", "3" if big_tile == "areg" else big_tile)
+def test_split_packing(pkg, preset, precision):
+    """Split-precision layers: the packed hi/lo planes reconstruct every weight to ~2^-16
+    (bf16x3) / ~2^-22 (f16x3, after the layer's 2^-ew) relative, in the fragment order of
+    conv_bf16x3.hip (tile 5 for the layer convs of M >= 128, tiles 1 / 2 below)."""
     cfg = C.PRESETS[preset]
     sd = C.make_state_dict(cfg, seed=31)
-    h = host_handle(pkg, cfg, "bf16x3")
+    h = host_handle(pkg, cfg, precision)
     for k, v in sd.items():
         h.set_weight(k, torch.from_numpy(v))
     h.commit()
@@ -236,8 +252,10 @@ def test_bf16x3_packing(pkg, preset, big_tile, monkeypatch):
         n_g, n_tg = -(-cin // 16), -(-k // TPC)
         assert info["n_chunks"] == n_g * n_tg
         u = packed.view(np.uint16).reshape(info["m_tiles"], n_g, n_tg, TPC, 2, wm_, WM, 64, 8)
-        hi = bf2f(u[:, :, :, :, 0])
-        lo = bf2f(u[:, :, :, :, 1])
+        hi = dec(u[:, :, :, :, 0], precision, info["ew"])
+        lo = dec(u[:, :, :, :, 1], precision, info["ew"])
+        if precision == "f16x3":  # the layer's max |w| lands in [2^14, 2^15) of f16
+            assert 2.0 ** 14 <= np.abs(W).max() * 2.0 ** info["ew"] < 2.0 ** 15, mod
         rec = np.zeros((info["m_tiles"] * MT, n_g * 16, n_tg * TPC), np.float64)
         lane = np.arange(64)
         for mt in range(info["m_tiles"]):
@@ -254,12 +272,12 @@ def test_bf16x3_packing(pkg, preset, big_tile, monkeypatch):
                                     rec[rows, cis, tg * TPC + jj] = val
         rec = rec[:cout, :cin, :k]
         err = np.abs(rec - W).max() / np.abs(W).max()
-        assert err < 2.0 ** -15, (mod, err)
+        assert err < SPLIT_TOL[precision], (mod, err)
         assert np.array_equal(bias[:cout], sd[mod + ".bias"])
     assert n_checked >= 2
 
 
-def unpack_bf16x3(info, packed, waves):
+def unpack_bf16x3(info, packed, waves, precision="bf16x3"):
     """Invert conv_bf16x3's fragment order → Wt[row][ci][tap] (hi + lo, float64)."""
     wm_, WM, TPC = waves
     MT = info["MT"]
@@ -267,7 +285,7 @@ def unpack_bf16x3(info, packed, waves):
     n_tg = -(-KT // TPC)
     n_g = n_chunks // n_tg
     u = packed.view(np.uint16).reshape(info["m_tiles"], n_g, n_tg, TPC, 2, wm_, WM, 64, 8)
-    val = bf2f(u[:, :, :, :, 0]).astype(np.float64) + bf2f(u[:, :, :, :, 1])
+    val = dec(u[:, :, :, :, 0], precision, info["ew"]) + dec(u[:, :, :, :, 1], precision, info["ew"])
     Wt = np.zeros((info["m_tiles"] * MT, n_g * 16, n_tg * TPC))
     lane = np.arange(64)
     for mt in range(info["m_tiles"]):
@@ -283,10 +301,11 @@ def unpack_bf16x3(info, packed, waves):
     return Wt[: info["M"], :, :KT]
 
 
-def test_bf16x3_polyphase_upsampler_packing(pkg):
+@pytest.mark.parametrize("precision", ["bf16x3", "f16x3"])
+def test_split_polyphase_upsampler_packing(pkg, precision):
     cfg = C.NONEXACT  # odd k-u on the first stages
     sd = C.make_state_dict(cfg, seed=41)
-    h = host_handle(pkg, cfg, "bf16x3")
+    h = host_handle(pkg, cfg, precision)
     for k, v in sd.items():
         h.set_weight(k, torch.from_numpy(v))
     h.commit()
@@ -297,7 +316,7 @@ def test_bf16x3_polyphase_upsampler_packing(pkg):
         info, packed, bias = h.packed_layer(f"ups.{i}")
         cin, cout = c0 >> i, c0 >> (i + 1)
         assert info["kind"] == 1 and info["CK"] == 16
-        Wt = unpack_bf16x3(info, packed, waves[info["tile"]])[:, :cin]
+        Wt = unpack_bf16x3(info, packed, waves[info["tile"]], precision)[:, :cin]
         x = rng.standard_normal((cin, 9)).astype(np.float32)
         ref = F.conv_transpose1d(torch.from_numpy(x)[None], torch.from_numpy(sd[f"ups.{i}.weight"]),
                                  torch.from_numpy(sd[f"ups.{i}.bias"]), u, (k - u) // 2)[0].numpy()
@@ -330,15 +349,16 @@ def _conv_same(x, w, b, d):
     return out
 
 
+@pytest.mark.parametrize("precision", ["bf16x3", "f16x3"])
 @pytest.mark.parametrize("preset", ["v1", "v2star"])
-def test_resblock_stream_packing_and_windowing(pkg, preset):
+def test_resblock_stream_packing_and_windowing(pkg, preset, precision):
     """Whole-ResBlock launches (resblock_bf16x3.hip) of the narrow stages: the packed A
     stream decodes (hi + lo, permuted channel slots) to every conv's weights, and the
     kernel's windowing (NWIN-column windows, garbage edges, centre W = NWIN - 2*halo,
     zero outside [0, len)) reproduces the un-windowed ResBlock, emulated in float64."""
     cfg = C.PRESETS[preset]
     sd = C.make_state_dict(cfg, seed=43)
-    h = host_handle(pkg, cfg, "bf16x3")
+    h = host_handle(pkg, cfg, precision)
     for k, v in sd.items():
         h.set_weight(k, torch.from_numpy(v))
     h.commit()
@@ -365,11 +385,12 @@ def test_resblock_stream_packing_and_windowing(pkg, preset):
             lane = np.arange(64)
             # resblock: [wave_m][conv][g][tap][plane][lane][8]
             u = packed.view(np.uint16).reshape(Cc // 32, n_conv, Cc // 16, KT, 2, 64, 8)
-            val = bf2f(u[:, :, :, :, 0]).astype(np.float64) + bf2f(u[:, :, :, :, 1])
             Ws = []
             for e in range(n_conv):
                 m, second = divmod(e, 2)
                 mod = f"mrfs.{i}.resblocks.{j}.convs{2 if second else 1}.{m}"
+                ew = h.packed_layer(mod)[0]["ew"]
+                val = dec(u[:, :, :, :, 0], precision, ew) + dec(u[:, :, :, :, 1], precision, ew)
                 W = sd[mod + ".weight"].astype(np.float64)
                 rec = np.zeros_like(W)
                 for wm in range(Cc // 32):
@@ -378,7 +399,7 @@ def test_resblock_stream_packing_and_windowing(pkg, preset):
                         for el in range(8):
                             ci = g * 16 + 4 * (lane >> 5) + (el & 3) + 8 * (el >> 2)
                             rec[rows, ci, :] = val[wm, e, g, :, lane, el]
-                assert np.abs(rec - W).max() <= 2.0 ** -15 * np.abs(W).max(), mod
+                assert np.abs(rec - W).max() <= SPLIT_TOL[precision] * np.abs(W).max(), mod
                 assert np.array_equal(bias[e * Cc:(e + 1) * Cc], sd[mod + ".bias"])
                 Ws.append((rec, sd[mod + ".bias"].astype(np.float64)))
             # windowed emulation vs direct, on one short utterance (len < L)
@@ -419,14 +440,12 @@ def _bf16_rne(a):
     return r.view(np.float32)
 
 
-@pytest.mark.parametrize("big_tile", ["0", "3"])
 @pytest.mark.parametrize("preset", ["v1", "v2star"])
-def test_bf16w_packing(pkg, preset, big_tile, monkeypatch):
+def test_bf16w_packing(pkg, preset):
     """HFG_DTYPE_BF16W: every conv weight is rounded to bf16 (nearest-even) when committed —
-    the split layers' lo planes are all zero and their hi planes are exactly bf16(W); the
-    fp32 layers (conv_post, C < 32 stages) hold the same bf16-valued weights; biases stay
-    fp32; the wide 8-wave tile (no NP 2 instance) is never chosen."""
-    monkeypatch.setenv("HFG_BF16X3_BIGTILE", big_tile)
+    the split layers (f16 halves of w 2^ew) have all-zero lo planes and hi planes exactly
+    bf16(W) 2^ew (8 significant bits fit f16's 11); the fp32 layers (conv_post, C < 32
+    stages) hold the same bf16-valued weights; biases stay fp32."""
     cfg = C.PRESETS[preset]
     sd = C.make_state_dict(cfg, seed=41)
     h = host_handle(pkg, cfg, "bf16w")
@@ -450,7 +469,7 @@ def test_bf16w_packing(pkg, preset, big_tile, monkeypatch):
             TPC = {0: 4, 1: 2, 2: 4, 3: 2, 4: 4, 5: 2}[info["tile"]]
             planes = u.reshape(-1, TPC, 2, u.size // (info["m_tiles"] * info["n_chunks"] * TPC * 2))
             assert not planes[:, :, 1].any(), f"{mod}: lo plane not zero"
-            hi = np.sort(bf2f(planes[:, :, 0]).ravel())
+            hi = np.sort(dec(planes[:, :, 0], "bf16w", info["ew"]).astype(np.float32).ravel())
             ref = np.sort(np.concatenate([_bf16_rne(W).ravel(),
                                           np.zeros(hi.size - W.size, np.float32)]))
             assert np.array_equal(hi, ref), mod

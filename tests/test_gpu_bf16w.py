@@ -1,13 +1,13 @@
 """bf16 weight storage (HFG_DTYPE_BF16W) on the GPU.
 
 bf16w rounds every conv weight to bf16 when the weights are committed; activations are
-still split hi + lo, so the kernels run hi(w)*hi(x) + hi(w)*lo(x) — the NP = 2
-instances of the bf16x3 kernels, which skip the lo(w)*hi(x) MFMA whose A operand is now
-all zero.  Two checks:
+still split hi + lo (the f16x3 format: power-of-two-scaled f16 halves), so the kernels run
+hi(w)*hi(x) + hi(w)*lo(x) — the NP = 2 instances of the f16x3 kernels, which skip the
+lo(w)*hi(x) MFMA (a bf16 value's 8 significant bits fit f16's 11, so lo(w) = 0).  Two checks:
 
 * against the oracle run on the bf16-rounded weights at the north-star 1e-4 (the model
   bf16w computes is the reference Generator with bf16-cast weights, not the fp32 one);
-* bitwise against the bf16x3 path fed the same pre-rounded weights: there every skipped
+* bitwise against the f16x3 path fed the same pre-rounded weights: there every skipped
   MFMA adds exactly 0 to the accumulator, so dropping it cannot change a bit.
 """
 import pytest
@@ -38,7 +38,7 @@ def _gen(pkg, cfg, state, dev, precision):
 @pytest.mark.parametrize("preset,B,T,lens", [("v1", 2, 120, [120, 77]), ("v1", 1, 48, None),
                                               ("v2star", 3, 64, [64, 31, 50]),
                                               ("nonexact", 2, 40, None)])
-def test_bf16w_vs_oracle_and_bf16x3(pkg, dev, preset, B, T, lens):
+def test_bf16w_vs_oracle_and_f16x3(pkg, dev, preset, B, T, lens):
     from oracle import config as C, hifigan_torch as H
     cfg = C.PRESETS[preset]
     sd = C.make_state_dict(cfg, seed=51)
@@ -48,7 +48,7 @@ def test_bf16w_vs_oracle_and_bf16x3(pkg, dev, preset, B, T, lens):
     rounded = _round_weights(sd)
     with torch.no_grad():
         w = _gen(pkg, cfg, fp32_state, dev, "bf16w")(mel.to(dev), **kw)
-        x3 = _gen(pkg, cfg, rounded, dev, "bf16x3")(mel.to(dev), **kw)
+        x3 = _gen(pkg, cfg, rounded, dev, "f16x3")(mel.to(dev), **kw)
     torch.cuda.synchronize()
     assert torch.equal(w, x3), (w - x3).abs().max().item()
     ref = H.generator_forward(rounded, cfg, mel)

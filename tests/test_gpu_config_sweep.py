@@ -46,7 +46,7 @@ def dev():
 
 @pytest.mark.parametrize("seed", range(N_CFG))
 def test_random_config(pkg, dev, seed):
-    """fp32 and bf16x3 against the oracle on the fp32 weights; bf16w against the oracle on
+    """fp32, f16x3 and bf16x3 against the oracle on the fp32 weights; bf16w against the oracle on
     the bf16-rounded weights (the model bf16w computes); every third configuration loads
     its weights in the apply_weight_norm layout (weight_g / weight_v)."""
     from oracle import config as C, hifigan_torch as H
@@ -70,7 +70,7 @@ def test_random_config(pkg, dev, seed):
         refs_by[name] = [H.generator_forward(H.to_torch_state(w), cfg, mel[b:b + 1, :, :n])
                          for b, n in enumerate(lens)]
     print(f"\nseed {seed}: {cfg} lens {lens} weight_norm {wn}")
-    for precision in ("fp32", "bf16x3", "bf16w"):
+    for precision in ("fp32", "f16x3", "bf16x3", "bf16w"):
         refs = refs_by["bf16" if precision == "bf16w" else "fp32"]
         gen = pkg.HiFiGANGenerator(**cfg.kwargs(), precision=precision).eval()
         if wn:

@@ -56,7 +56,7 @@ def test_world2_vocode_sharded_bitwise(dev):
     res = _last_json(r.stdout)
     print("\n" + json.dumps(res, indent=1))
     assert res["world"] == 2
-    assert set(res["checks"]) == {"C3_v1_64x80x1024/bf16x3", "C5_sambert_b32/bf16x3",
+    assert set(res["checks"]) == {"C3_v1_64x80x1024/f16x3", "C5_sambert_b32/f16x3",
                                   "C5_sambert_b32/fp32"}
     for name, chk in res["checks"].items():
         assert chk["bitwise_vs_single_process"], name

@@ -16,7 +16,7 @@ def dev():
     return torch.device("cuda:0")
 
 
-@pytest.fixture(scope="module", params=["fp32", "bf16x3"])
+@pytest.fixture(scope="module", params=["fp32", "f16x3"])
 def gen_sd(pkg, dev, request):
     from oracle import config as C
     sd = C.make_state_dict(C.V1, seed=4)
@@ -94,12 +94,12 @@ def test_streaming_equals_one_shot(pkg, gen_sd, dev):
     assert torch.equal(out, ref)
 
 
-@pytest.mark.parametrize("precision", ["fp32", "bf16x3", "bf16w"])
+@pytest.mark.parametrize("precision", ["fp32", "f16x3", "bf16x3", "bf16w"])
 @pytest.mark.parametrize("preset", ["v1", "v2star", "nonexact"])
 def test_ragged_sweep_equals_solo(pkg, dev, preset, precision):
     """Ragged batches of random lengths (1, odd, even; garbage in the padding) in both mel
     layouts, for every config family and precision: each item bitwise equal to the
-    utterance run alone, zero past its length, and (fp32 / bf16x3) within 1e-4 of the
+    utterance run alone, zero past its length, and (fp32 / f16x3 / bf16x3) within 1e-4 of the
     oracle.  Covers every execution schedule a length mix selects (small-grid tile,
     concurrent ResBlocks + mrf_combine, thin stages, 2-stream split)."""
     from oracle import config as C, hifigan_torch as H
@@ -172,7 +172,7 @@ def test_ten_minute_stream_constant_memory(pkg, dev):
     glue = importlib.import_module("tts_sambert_hifigan_amd.glue")
     from oracle import config as C
     sd = C.make_state_dict(C.V1, seed=4)
-    gen = pkg.HiFiGANGenerator(**C.V1.kwargs(), precision="bf16x3").eval()
+    gen = pkg.HiFiGANGenerator(**C.V1.kwargs(), precision="f16x3").eval()
     gen.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
     gen = gen.to(dev)
     T = 22050 * 600 // 256

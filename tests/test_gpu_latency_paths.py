@@ -1,6 +1,6 @@
 """Small-batch launch paths on the GPU (VERDICT r01 "small-batch latency").
 
-A bf16x3 layer launch whose tile-3 grid would leave most CUs idle runs on the 64x64
+A split-precision layer launch whose tile-3 grid would leave most CUs idle runs on the 64x64
 small-grid tile (kernels.h, tile 4; HFG_SMALL_TILE=-1 auto / 0 never / 1 always).  Every
 output element sees the same MFMA sequence on either tile, so the choice must be bitwise
 invisible: forced-small, forced-big and auto forwards are compared with torch.equal,
@@ -39,15 +39,16 @@ def _gen(pkg, cfg, sd, dev, precision, env):
     return gen
 
 
+@pytest.mark.parametrize("precision", ["f16x3", "bf16x3"])
 @pytest.mark.parametrize("preset,B,T", [("v1", 1, 96), ("v1", 3, 40), ("v2star", 2, 64), ("v1", 2, 300)])
-def test_small_tile_is_bitwise_invisible(pkg, dev, preset, B, T):
+def test_small_tile_is_bitwise_invisible(pkg, dev, preset, B, T, precision):
     from oracle import config as C, hifigan_torch as H
     cfg = C.PRESETS[preset]
     sd = C.make_state_dict(cfg, seed=31)
     mel = torch.randn(B, 80, T, generator=torch.Generator().manual_seed(B * T))
     outs = {}
     for mode in ("0", "1", "-1"):
-        gen = _gen(pkg, cfg, sd, dev, "bf16x3", {"HFG_SMALL_TILE": mode})
+        gen = _gen(pkg, cfg, sd, dev, precision, {"HFG_SMALL_TILE": mode})
         with torch.no_grad():
             outs[mode] = gen(mel.to(dev))
         torch.cuda.synchronize()
@@ -64,7 +65,7 @@ def test_small_tile_ragged_and_streaming(pkg, dev):
     from oracle import config as C
     cfg = C.V1
     sd = C.make_state_dict(cfg, seed=32)
-    gen = _gen(pkg, cfg, sd, dev, "bf16x3", {"HFG_SMALL_TILE": "-1"})
+    gen = _gen(pkg, cfg, sd, dev, "f16x3", {"HFG_SMALL_TILE": "-1"})
     lens = [40, 7, 33]
     mel = torch.randn(3, 80, 40, generator=torch.Generator().manual_seed(5))
     with torch.no_grad():
@@ -74,7 +75,7 @@ def test_small_tile_ragged_and_streaming(pkg, dev):
             assert torch.equal(wav[b:b + 1, :, :n * 256], solo), b
 
 
-@pytest.mark.parametrize("precision", ["bf16x3", "fp32"])
+@pytest.mark.parametrize("precision", ["f16x3", "bf16x3", "fp32"])
 @pytest.mark.parametrize("preset,B,T", [("v1", 1, 96), ("v1", 4, 50), ("v2star", 2, 64)])
 def test_concurrent_resblocks_are_bitwise_invisible(pkg, dev, precision, preset, B, T):
     """HFG_RB_CONC: the ResBlocks of an MRF on concurrent streams, each into its own
@@ -100,7 +101,7 @@ def test_concurrent_resblocks_hipgraph(pkg, dev):
     from oracle import config as C
     cfg = C.V1
     sd = C.make_state_dict(cfg, seed=34)
-    gen = _gen(pkg, cfg, sd, dev, "bf16x3", {"HFG_RB_CONC": "1"})
+    gen = _gen(pkg, cfg, sd, dev, "f16x3", {"HFG_RB_CONC": "1"})
     gen.verify_weights = False
     mel = torch.randn(1, 80, 64, generator=torch.Generator().manual_seed(2)).to(dev)
     with torch.no_grad():
@@ -118,28 +119,7 @@ def test_concurrent_resblocks_hipgraph(pkg, dev):
     assert torch.equal(out, eager)
 
 
-@pytest.mark.parametrize("precision", ["bf16x3", "fp32"])
-def test_lds_staged_epilogue_is_bitwise_invisible(pkg, dev, precision):
-    """HFG_EPI_LDS=1: the bf16x3 layer kernels' epilogue staged through LDS with float4
-    stores (epilogue.h conv_epilogue_lds) — the same additions in the same order as the
-    accumulator-layout epilogue, so the wav is bitwise unchanged (residual, lrelu and MRF
-    running-sum modes all occur in a V1 forward)."""
-    from oracle import config as C
-    cfg = C.V1
-    sd = C.make_state_dict(cfg, seed=35)
-    mel = torch.randn(2, 80, 200, generator=torch.Generator().manual_seed(9))
-    outs = {}
-    for mode in ("0", "1"):
-        gen = _gen(pkg, cfg, sd, dev, precision, {"HFG_EPI_LDS": mode, "HFG_SMALL_TILE": "0",
-                                                  "HFG_RB_CONC": "0"})
-        with torch.no_grad():
-            outs[mode] = gen(mel.to(dev), lengths=[200, 141])
-        torch.cuda.synchronize()
-    assert torch.equal(outs["0"], outs["1"])
-
-
-
-@pytest.mark.parametrize("precision", ["fp32", "bf16x3"])
+@pytest.mark.parametrize("precision", ["fp32", "f16x3", "bf16x3"])
 @pytest.mark.parametrize("preset", ["nonexact", "v1"])
 def test_ragged_batch_with_concurrent_resblocks_equals_solo(pkg, dev, preset, precision):
     """A ragged batch whose stage lengths are not multiples of 4 (non-exact upsampling:
@@ -163,32 +143,17 @@ def test_ragged_batch_with_concurrent_resblocks_equals_solo(pkg, dev, preset, pr
     torch.cuda.synchronize()
 
 
-@pytest.mark.parametrize("preset,B,T", [("v1", 2, 200), ("v1", 1, 96), ("v2star", 2, 64)])
-def test_areg_tile_is_bitwise_invisible(pkg, dev, preset, B, T):
-    """HFG_AREG=1: tile-3 layer convs on tile 5 (A fragments from global into registers,
-    one barrier per channel group; kernels.h) — the same MFMA sequence per output
-    element, so the wav is bitwise unchanged."""
-    from oracle import config as C
-    cfg = C.PRESETS[preset]
-    sd = C.make_state_dict(cfg, seed=36)
-    mel = torch.randn(B, 80, T, generator=torch.Generator().manual_seed(11))
-    outs = {}
-    for mode in ("0", "1"):
-        gen = _gen(pkg, cfg, sd, dev, "bf16x3", {"HFG_AREG": mode, "HFG_SMALL_TILE": "0"})
-        with torch.no_grad():
-            outs[mode] = gen(mel.to(dev), lengths=[T - 7 * b for b in range(B)])
-        torch.cuda.synchronize()
-    assert torch.equal(outs["0"], outs["1"])
-
-
-@pytest.mark.parametrize("precision", ["bf16x3", "bf16w"])
+@pytest.mark.parametrize("precision", ["bf16x3", "f16x3", "bf16w"])
 @pytest.mark.parametrize("preset", ["v1", "nonexact"])
 def test_split_resblock_is_bitwise_invisible(pkg, dev, preset, precision):
     """HFG_RB_SPLIT=1 (default): a whole-ResBlock launch whose halo recompute the split cuts
     by >= 10 % (k = 11 at C = 32 / 64 in V1) runs as two launches — dilation pairs {1, 3}
     writing x to scratch, then {5} with the MRF epilogue — each window paying only its own
-    halo.  The fp32 round trip of x is exact, so the wav is bitwise unchanged (ragged batch,
-    and the standalone MRF / ResBlock entry points through the same path)."""
+    halo.  The fp32 round trip of x is exact, so the bf16x3 wav is bitwise unchanged (ragged
+    batch, and the standalone MRF / ResBlock entry points through the same path).  f16x3 /
+    bf16w scale each operand by its block's largest |value|, and the second launch's windows
+    differ: only values whose f16 lo half falls below the normal range (< 2^-17 of the
+    window's max) can round differently, so the two schedules agree to ~1e-9 of the wav."""
     from oracle import config as C
     cfg = C.PRESETS[preset]
     sd = C.make_state_dict(cfg, seed=40)
@@ -201,5 +166,11 @@ def test_split_resblock_is_bitwise_invisible(pkg, dev, preset, precision):
             outs[mode] = gen(mel.to(dev), lengths=[150, 97, 31])
             outs[mode + "c"] = conc(mel[:1].to(dev))  # concurrent ResBlocks, per-part scratch
         torch.cuda.synchronize()
-    assert torch.equal(outs["0"], outs["1"])
-    assert torch.equal(outs["0c"], outs["1c"])
+    if precision == "bf16x3":
+        assert torch.equal(outs["0"], outs["1"])
+        assert torch.equal(outs["0c"], outs["1c"])
+    else:
+        for k in ("", "c"):
+            d = (outs["0" + k] - outs["1" + k]).abs().max().item()
+            print(f"\n{preset} [{precision}] split vs one launch{' (conc)' if k else ''}: {d:.2e}")
+            assert d <= 1e-7

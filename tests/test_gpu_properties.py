@@ -214,29 +214,29 @@ def test_hipgraph_capture_replay(v1, dev):
     assert not torch.equal(out, ref)
 
 
-# ---- full size, headline precision (bf16x3, 2 streams: what bench.py times) -------
+# ---- full size, headline precision (f16x3, 2 streams: what bench.py times) -------
 @pytest.fixture(scope="module")
-def full_bf16x3(pkg, full, dev):
+def full_split(pkg, full, dev):
     from oracle import config as C
     _, sd, mel, wav32 = full
-    gen = pkg.HiFiGANGenerator(**C.V1.kwargs(), precision="bf16x3").eval()
+    gen = pkg.HiFiGANGenerator(**C.V1.kwargs(), precision="f16x3").eval()
     gen.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
     gen = gen.to(dev)
     return gen, sd, mel, run(gen, mel.to(dev)), wav32
 
 
-def test_full_size_bf16x3_vs_fp32_path(full_bf16x3):
+def test_full_size_split_vs_fp32_path(full_split):
     """At the bench size ([8,80,1024]) the split-precision path stays within the
     north_star tolerance of the exact-fp32 path on every sample of every utterance."""
-    _, _, _, wav, wav32 = full_bf16x3
+    _, _, _, wav, wav32 = full_split
     assert (wav - wav32).abs().max().item() < ATOL
 
 
 @pytest.mark.parametrize("item,start", [(1, 0), (6, 700), (4, 1024 - 48)])
-def test_full_size_bf16x3_windowed_oracle(full_bf16x3, item, start):
-    """bf16x3 full-size output against the oracle on a receptive-field window."""
+def test_full_size_split_windowed_oracle(full_split, item, start):
+    """f16x3 full-size output against the oracle on a receptive-field window."""
     from oracle import config as C, hifigan_torch as H
-    _, sd, mel, wav, _ = full_bf16x3
+    _, sd, mel, wav, _ = full_split
     W, M = 48, 16
     a, b = max(0, start - M), min(1024, start + W + M)
     ref = H.generator_forward(H.to_torch_state(sd), C.V1, mel[item:item + 1, :, a:b])
@@ -245,10 +245,10 @@ def test_full_size_bf16x3_windowed_oracle(full_bf16x3, item, start):
     assert np.abs(got - ref).max() < ATOL
 
 
-def test_full_size_bf16x3_batch_split_invariance(full_bf16x3, dev):
+def test_full_size_split_batch_split_invariance(full_split, dev):
     """Utterances are independent on the headline path too (bitwise), whatever the
     batch composition and stream split."""
-    gen, _, mel, wav, _ = full_bf16x3
+    gen, _, mel, wav, _ = full_split
     one = run(gen, mel[3:4].to(dev))
     assert torch.equal(one[0], wav[3])
     five = run(gen, mel[1:6].to(dev))
@@ -259,7 +259,7 @@ def test_full_size_bf16x3_batch_split_invariance(full_bf16x3, dev):
 T_MAX = 131071  # V1: 8192 * T fp32 per item < 2^30 elements, the kernels' 32-bit byte offsets
 
 
-@pytest.mark.parametrize("precision", ["bf16x3", "fp32"])
+@pytest.mark.parametrize("precision", ["f16x3", "bf16x3", "fp32"])
 def test_max_length_utterance_windowed_oracle(pkg, dev, precision):
     """One utterance at the longest T the C ABI accepts (2^30 - 8192 activation elements per
     item, ~25 min of audio): the output at the head, the middle and the very end matches

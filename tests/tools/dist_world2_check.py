@@ -40,7 +40,7 @@ def main():
     gd = os.path.join(ROOT, "tests", "golden")
     meta = json.load(open(os.path.join(gd, "golden_c5.json")))
     arr = np.load(os.path.join(gd, "c5_sambert_b32.npz"))
-    for precision in ("bf16x3", "fp32"):
+    for precision in ("f16x3", "fp32"):
         cfg = C.V1
         spec = [(k, s) for k, s, _ in C.param_specs(cfg)]
         sd0 = ({k: torch.from_numpy(v) for k, v in
@@ -50,7 +50,7 @@ def main():
         gen.load_state_dict(sd)
         gen = gen.to(dev)
         cases = {}
-        if precision == "bf16x3":
+        if precision == "f16x3":
             g = torch.Generator().manual_seed(1234)
             cases["C3_v1_64x80x1024"] = (torch.randn(64, 80, 1024, generator=g), None, "bct")
         mel_pred = torch.from_numpy(arr["mel_pred"])

@@ -60,7 +60,7 @@ class HfgConfig(ctypes.Structure):
     ]
 
 
-DTYPES = {"fp32": 0, "bf16x3": 1, "bf16w": 2}
+DTYPES = {"fp32": 0, "bf16x3": 1, "bf16w": 2, "f16x3": 3}
 
 
 class HfgMrfConfig(ctypes.Structure):
@@ -353,13 +353,13 @@ class Handle:
     def packed_layer(self, mod: str):
         """(info dict, packed weights np.ndarray, per-row bias np.ndarray) of one layer."""
         import numpy as np
-        info = (c_int64 * 10)()
+        info = (c_int64 * 11)()
         check(self.lib.hfg_debug_packed_layer(self.ptr, mod.encode(), None, 0, info))
         w_len, b_len = int(info[6]), int(info[7])
         out = np.zeros(w_len + b_len, dtype=np.float32)
         check(self.lib.hfg_debug_packed_layer(
             self.ptr, mod.encode(), out.ctypes.data_as(POINTER(c_float)), out.size, info))
-        keys = ["kind", "M", "KT", "tile", "m_tiles", "n_chunks", "w_len", "b_len", "CK", "MT"]
+        keys = ["kind", "M", "KT", "tile", "m_tiles", "n_chunks", "w_len", "b_len", "CK", "MT", "ew"]
         return dict(zip(keys, [int(v) for v in info])), out[:w_len], out[w_len:]
 
     def packed_resblock(self, stage: int, j: int):

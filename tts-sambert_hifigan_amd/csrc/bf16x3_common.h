@@ -1,6 +1,25 @@
 // bf16x3_common.h — pieces shared by the split-precision conv kernels
 // (conv_bf16x3.hip: one Conv1d / polyphase ConvTranspose1d per launch;
-//  resblock_bf16x3.hip: a whole ResBlock, all dilations, per launch).
+//  resblock_bf16x3.hip: a whole ResBlock, all dilations, per launch;
+//  ups_bf16x3.hip, mrf_thin_mfma.hip).
+//
+// Split formats (template parameter FMT of every split kernel):
+//   kFmtBf16 (bf16x3): hi = bf16(v), lo = bf16(v - hi); hi*hi + hi*lo + lo*hi in fp32 on the
+//     bf16 matrix cores: ~16-bit-mantissa products.
+//   kFmtF16 (f16x3): the same three products of f16 halves of a power-of-two SCALED operand:
+//     hi = f16(v * 2^e), lo = f16(v * 2^e - hi) carry 22 significant bits, so a product misses
+//     the exact one by <= ~3 * 2^-22 relative — fp32-class (an fp32 product rounds at 2^-24,
+//     and the fp32 accumulation both modes share adds more than the split does).  f16 has 5
+//     exponent bits, so every operand is scaled by a power of two into [2^14, 2^15) of its
+//     tensor's (activations) or layer's (weights) largest magnitude; the scales are exact, the
+//     accumulator is multiplied by 2^-(e_x + e_w) after the main loop, and a value the scaling
+//     leaves below the f16 normal range (< 2^-17 of that largest magnitude) keeps an absolute
+//     error <= 2^-39 of it.  The f16 MFMAs run at the bf16 rate (MI355X_MICROARCH.md).
+//   Activation scales come from the producing launch: its epilogue folds max|stored value| of
+//   each batch item into a per-(launch, item) slot (amax_commit); the consuming launch reads
+//   the slot of its input (per item: a batch item's result does not depend on the others).  A
+//   whole-ResBlock / whole-MRF kernel scales the operands it forms internally per block
+//   (block_amax).
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -14,6 +33,71 @@ typedef floatx16e floatx16;
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __attribute__((address_space(3))) void* lds_ptr_t3;
 typedef __attribute__((address_space(1))) void* gptr_t1;
+
+
+typedef _Float16 halfx8 __attribute__((ext_vector_type(8)));
+typedef _Float16 halfx4_ __attribute__((ext_vector_type(4)));
+typedef _Float16 halfx2_ __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2_ __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x4_ __attribute__((ext_vector_type(4)));
+typedef float floatx2_ __attribute__((ext_vector_type(2)));
+typedef float floatx4_ __attribute__((ext_vector_type(4)));
+
+// Fragments are carried as bf16x8 bit patterns in both formats (16 bytes); the MFMA
+// wrappers reinterpret them for the f16 instructions.
+template <int FMT>
+__device__ __forceinline__ floatx16 mfma32(const bf16x8& a, const bf16x8& b, const floatx16& c) {
+  if constexpr (FMT == kFmtBf16)
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+  else
+    return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(halfx8, a),
+                                                  __builtin_bit_cast(halfx8, b), c, 0, 0, 0);
+}
+template <int FMT>
+__device__ __forceinline__ floatx4_ mfma16(const bf16x8& a, const bf16x8& b, const floatx4_& c) {
+  if constexpr (FMT == kFmtBf16)
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+  else
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(halfx8, a),
+                                                  __builtin_bit_cast(halfx8, b), c, 0, 0, 0);
+}
+
+// hi = fmt(a), lo = fmt(a - hi) of two values (a - hi is exact in fp32), as bit patterns
+template <int FMT>
+__device__ __forceinline__ void split2(const floatx2_& a, bf16x2_& hi, bf16x2_& lo) {
+  if constexpr (FMT == kFmtBf16) {
+    hi = __builtin_convertvector(a, bf16x2_);
+    const floatx2_ hf = __builtin_convertvector(hi, floatx2_);
+    lo = __builtin_convertvector(a - hf, bf16x2_);
+  } else {
+    const halfx2_ h = __builtin_convertvector(a, halfx2_);
+    const floatx2_ hf = __builtin_convertvector(h, floatx2_);
+    const halfx2_ l = __builtin_convertvector(a - hf, halfx2_);
+    hi = __builtin_bit_cast(bf16x2_, h);
+    lo = __builtin_bit_cast(bf16x2_, l);
+  }
+}
+
+// f16x3 scale exponent e for values with |v| <= m: m * 2^e in [2^14, 2^15) (max f16 65504),
+// clamped to +-kX3ExpMax so 2^-(e_x + e_w) stays a normal float; 0 for m = 0 / inf / NaN
+__device__ __forceinline__ int x3_exp(float m) {
+  if (!(m > 0.f) || !(m <= 3.0e38f)) return 0;
+  const int e = 15 - __builtin_amdgcn_frexp_expf(m);  // m = f 2^x, f in [0.5, 1)
+  return e < -kX3ExpMax ? -kX3ExpMax : (e > kX3ExpMax ? kX3ExpMax : e);
+}
+// 2^e as a float, |e| <= 126
+__device__ __forceinline__ float exp2i(int e) { return __builtin_bit_cast(float, (unsigned)(127 + e) << 23); }
+// scale exponent of item b's producer slot (slots null: no scaling): the max of its
+// kAmaxSpread words (amax_commit), all uniform loads
+__device__ __forceinline__ int x3_exp_slot(const uint32_t* slots, int b) {
+  if (!slots) return 0;
+  const uint32_t* s = slots + (size_t)b * kAmaxSpread;
+  uint32_t m = 0;
+#pragma unroll
+  for (int i = 0; i < kAmaxSpread; ++i) m = max(m, s[i]);
+  return x3_exp(__builtin_bit_cast(float, m));
+}
+
 
 // leaky_relu(v, 0.1) as max(v, 0.1 v): bitwise the reference's select (slope < 1), two
 // VALU ops (v_mul + v_max) instead of compare + multiply + select

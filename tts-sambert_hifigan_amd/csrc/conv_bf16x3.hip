@@ -55,7 +55,7 @@ typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 }  // namespace
 
 template <int KT_, int TPC, int WAVES_M, int WAVES_N, int WM, int WN, int WD, bool UPS, int NP,
-          bool AREG>
+          bool AREG, int FMT>
 __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N, 2)
 conv1d_bf16x3(const ConvParams p) {
   static_assert(!AREG || (KT_ > 0 && !UPS && WM * WN >= 8), "AREG: compile-time taps, layer convs");
@@ -136,6 +136,10 @@ conv1d_bf16x3(const ConvParams p) {
   if (n0 >= N_b) return;  // whole tile past this utterance's end (block-uniform)
   const int L_out_b = (UPS && p.len_out) ? p.len_out[b] : p.L_out;
   const int xcs = (int)p.x_cs, xts = (int)p.x_ts;
+  // f16x3 (bf16x3_common.h): the input's power-of-two scale from its producer's per-item max
+  // (folded into the staging factors below) and the accumulator's unscale after the loop
+  const int ex = FMT == kFmtF16 ? x3_exp_slot(p.amax_in, b) : 0;
+  const float sx = FMT == kFmtF16 ? exp2i(ex) : 1.0f;
   const int wbase = n0 + p.off;                   // input index of window row 0
 
   auto taps_in = [&](int c) {
@@ -198,7 +202,7 @@ conv1d_bf16x3(const ConvParams p) {
       const int i = tid + q * NT;
       const int t = i >> 1;
       // (ablation bit7: always re-read channel group 0, i.e. L2-warm loads)
-      const int cb = ((p.dbg & 128) ? 0 : g) * 16 + (i & 1) * 8;
+      const int cb = ((kAblate && (p.dbg & 128)) ? 0 : g) * 16 + (i & 1) * 8;
       const int gi = wbase + t;
       const bool tok = (i < 2 * XW) && ((unsigned)gi < (unsigned)L_in_b);
       // byte offsets from the block-uniform base: SGPR base + 32-bit VGPR offset loads
@@ -208,8 +212,8 @@ conv1d_bf16x3(const ConvParams p) {
       const int ecap = full ? 7 : min(p.C_in - 1 - cb, 7);
       const uint32_t m8 = tok ? (ecap >= 7 ? 0xffu : (ecap < 0 ? 0u : (1u << (ecap + 1)) - 1u)) : 0u;
       xok |= m8 << (q * 8);
-      xs1[q] = tok ? 1.0f : 0.0f;
-      xs2[q] = tok ? slope : 0.0f;
+      xs1[q] = tok ? sx : 0.0f;
+      xs2[q] = tok ? slope * sx : 0.0f;
       if (full) {
         // whole group: buffer loads with the channel step in the scalar offset (one offset
         // VGPR per row instead of eight); a lane outside the window reads channel e at
@@ -234,7 +238,7 @@ conv1d_bf16x3(const ConvParams p) {
       const int i = tid + q * NT;
       if (AREG || i < 2 * XW) {
         bf16x8 h, l;
-        if (UPS && (p.dbg & 256)) {
+        if (kAblate && UPS && (p.dbg & 256)) {
           // ablation (upsamplers, timing only): the raw fp32 halves, no pre-activation or split
 #pragma unroll
           for (int e = 0; e < 8; ++e) {
@@ -256,10 +260,10 @@ conv1d_bf16x3(const ConvParams p) {
               a[0] = lrelu3(a[0]);
               a[1] = lrelu3(a[1]);
             }
+            if constexpr (FMT == kFmtF16) a = a * sx;
           }
-          const bf16x2 hh = __builtin_convertvector(a, bf16x2);
-          const floatx2 hf = __builtin_convertvector(hh, floatx2);
-          const bf16x2 ll = __builtin_convertvector(a - hf, bf16x2);
+          bf16x2 hh, ll;
+          split2<FMT>(a, hh, ll);
           h[e] = hh[0];
           h[e + 1] = hh[1];
           l[e] = ll[0];
@@ -313,9 +317,9 @@ conv1d_bf16x3(const ConvParams p) {
 #pragma unroll
       for (int k = 0; k < WN; ++k) {
         if constexpr (NP == 3)  // the weights' lo plane (zero for bf16-valued weights: NP 2)
-          acc[i][k] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.al[i], f.bh[k], acc[i][k], 0, 0, 0);
-        acc[i][k] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.ah[i], f.bl[k], acc[i][k], 0, 0, 0);
-        acc[i][k] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.ah[i], f.bh[k], acc[i][k], 0, 0, 0);
+          acc[i][k] = mfma32<FMT>(f.al[i], f.bh[k], acc[i][k]);
+        acc[i][k] = mfma32<FMT>(f.ah[i], f.bl[k], acc[i][k]);
+        acc[i][k] = mfma32<FMT>(f.ah[i], f.bh[k], acc[i][k]);
       }
   };
 
@@ -344,9 +348,9 @@ conv1d_bf16x3(const ConvParams p) {
 #pragma unroll
       for (int i = 0; i < WM; ++i) {
         if constexpr (NP == 3)
-          acc[i][k] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[i], bh[k & 1], acc[i][k], 0, 0, 0);
-        acc[i][k] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bl[k & 1], acc[i][k], 0, 0, 0);
-        acc[i][k] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bh[k & 1], acc[i][k], 0, 0, 0);
+          acc[i][k] = mfma32<FMT>(al[i], bh[k & 1], acc[i][k]);
+        acc[i][k] = mfma32<FMT>(ah[i], bl[k & 1], acc[i][k]);
+        acc[i][k] = mfma32<FMT>(ah[i], bh[k & 1], acc[i][k]);
       }
     }
   };
@@ -441,9 +445,9 @@ conv1d_bf16x3(const ConvParams p) {
 #pragma unroll
         for (int i = 0; i < WM; ++i) {
           if constexpr (NP == 3)
-            acc[i][k] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1][i], bh[k & 1], acc[i][k], 0, 0, 0);
-          acc[i][k] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][i], bl[k & 1], acc[i][k], 0, 0, 0);
-          acc[i][k] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][i], bh[k & 1], acc[i][k], 0, 0, 0);
+            acc[i][k] = mfma32<FMT>(a[1][i], bh[k & 1], acc[i][k]);
+          acc[i][k] = mfma32<FMT>(a[0][i], bl[k & 1], acc[i][k]);
+          acc[i][k] = mfma32<FMT>(a[0][i], bh[k & 1], acc[i][k]);
         }
       }
     };
@@ -568,7 +572,7 @@ conv1d_bf16x3(const ConvParams p) {
         // the slab of chunk c+1 must have landed; younger: this chunk's input loads
         if (ISX && !STX) wait_x(std::integral_constant<int, NX>{});
         else wait_vm<0>();
-        if (!(p.dbg & 4)) lds_barrier();
+        if (!(kAblate && (p.dbg & 4))) lds_barrier();
         wslot ^= 1;
       }
     }
@@ -584,8 +588,8 @@ conv1d_bf16x3(const ConvParams p) {
     const __bf16* Ws = Wbuf0 + wslot * SLAB;
     const __bf16* Xh = Xbuf0 + (g & 1) * xbuf;
     const bool more_groups = (g + 1) * n_tg < p.n_chunks;
-    const bool issue_x = more_groups && tg == xg && !(p.dbg & 1);
-    const bool store_now = more_groups && tg == n_tg - 1 && !(p.dbg & 1);
+    const bool issue_x = more_groups && tg == xg && !(kAblate && (p.dbg & 1));
+    const bool store_now = more_groups && tg == n_tg - 1 && !(kAblate && (p.dbg & 1));
     // always PW pieces per thread, so every vmcnt below is a constant: past the last
     // chunk the last slab is re-read into the free slot (that of chunk c-1)
     auto issue_next_w = [&]() {
@@ -630,13 +634,21 @@ conv1d_bf16x3(const ConvParams p) {
     // consumes them.
     if (issue_x && !store_now) wait_x(std::integral_constant<int, NX + PW * (WD - 2)>{});
     else wait_vm<PW * (WD - 2)>();
-    if (!(p.dbg & 4)) lds_barrier();
+    if (!(kAblate && (p.dbg & 4))) lds_barrier();
     if (++wslot == WD) wslot = 0;
   }
   }
-  if (p.dbg & 8) {  // ablation: no epilogue
+  if (kAblate && (p.dbg & 8)) {  // ablation: no epilogue
     if (acc[0][0][0] == 1.2345e-30f) p.y[0] = acc[WM - 1][WN - 1][15];
     return;
+  }
+  if constexpr (FMT == kFmtF16) {
+    // products of 2^ex-scaled inputs and 2^ew-scaled weights: exact power-of-two unscale
+    const float inv = exp2i(-(ex + p.ew));
+#pragma unroll
+    for (int i = 0; i < WM; ++i)
+#pragma unroll
+      for (int k = 0; k < WN; ++k) acc[i][k] = acc[i][k] * inv;
   }
 
   // ---- epilogue (same contract as conv1d_mfma_f32) ----
@@ -653,6 +665,10 @@ conv1d_bf16x3(const ConvParams p) {
     const bool pow2 = (s_ & (s_ - 1)) == 0;
     const int sh = __builtin_ctz((unsigned)s_);
     auto co_of = [&](int row) { return pow2 ? row >> sh : row / s_; };
+    float vmax = 0.f;  // max |stored value| (f16x3 consumers: p.amax_out)
+    auto track4 = [&](const float4& v) {
+      vmax = fmaxf(vmax, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+    };
 #pragma unroll
     for (int i = 0; i < WM; ++i) {
       const int rb = mt * MT + wave_m * 32 * WM + i * 32 + 4 * half;  // row of r = 0
@@ -680,6 +696,7 @@ conv1d_bf16x3(const ConvParams p) {
             v.z = acc[i][k][4 * q + 2] + bv[4 * q + 2];
             v.w = acc[i][k][4 * q + 3] + bv[4 * q + 3];
             *reinterpret_cast<float4*>(yb + (int64_t)co * p.L_out + t) = v;
+            track4(v);
           }
           continue;
         }
@@ -699,11 +716,12 @@ conv1d_bf16x3(const ConvParams p) {
             float* dst = yb + (int64_t)co * p.L_out + t;
             if (t >= 0 && t + 3 < L_out_b) {
               *reinterpret_cast<float4*>(dst) = v;
+              track4(v);
             } else {
-              if (t + 0 >= 0 && t + 0 < L_out_b) dst[0] = v.x;
-              if (t + 1 >= 0 && t + 1 < L_out_b) dst[1] = v.y;
-              if (t + 2 >= 0 && t + 2 < L_out_b) dst[2] = v.z;
-              if (t + 3 >= 0 && t + 3 < L_out_b) dst[3] = v.w;
+              if (t + 0 >= 0 && t + 0 < L_out_b) dst[0] = v.x, vmax = fmaxf(vmax, fabsf(v.x));
+              if (t + 1 >= 0 && t + 1 < L_out_b) dst[1] = v.y, vmax = fmaxf(vmax, fabsf(v.y));
+              if (t + 2 >= 0 && t + 2 < L_out_b) dst[2] = v.z, vmax = fmaxf(vmax, fabsf(v.z));
+              if (t + 3 >= 0 && t + 3 < L_out_b) dst[3] = v.w, vmax = fmaxf(vmax, fabsf(v.w));
             }
           }
           continue;
@@ -714,10 +732,15 @@ conv1d_bf16x3(const ConvParams p) {
           if (row >= p.M) continue;
           const int co = co_of(row);
           const int t = n * s_ + (row - co * s_) - p_;
-          if (t >= 0 && t < L_out_b) yb[(int64_t)co * p.L_out + t] = acc[i][k][r] + bv[r];
+          if (t >= 0 && t < L_out_b) {
+            const float v = acc[i][k][r] + bv[r];
+            yb[(int64_t)co * p.L_out + t] = v;
+            vmax = fmaxf(vmax, fabsf(v));
+          }
         }
       }
     }
+    if (p.amax_out) amax_commit(vmax, p.amax_out, b);
   } else {
     // LDS-staged float4 epilogue (epilogue.h) when the rows are 16-B aligned and the host
     // sized the LDS for it (p.epi_lds); the accumulator-layout epilogue otherwise
@@ -741,11 +764,12 @@ namespace {
 
 typedef void (*ConvFn3)(const ConvParams);
 
-template <int KT, int TILE, bool UPS, int NP>
+template <int KT, int TILE, bool UPS, int NP, int FMT>
 struct Inst3 {
   static constexpr Bf16x3Cfg t = kBf16x3Tiles[TILE];
   static ConvFn3 fn() {
-    return conv1d_bf16x3<KT, t.TPC, t.WAVES_M, t.WAVES_N, t.WM, t.WN, t.WD, UPS, NP, t.AREG != 0>;
+    return conv1d_bf16x3<KT, t.TPC, t.WAVES_M, t.WAVES_N, t.WM, t.WN, t.WD, UPS, NP, t.AREG != 0,
+                         FMT>;
   }
 };
 
@@ -753,22 +777,25 @@ struct Entry3 {
   int kt;
   int tile;
   bool ups;
-  int np;
+  int np, fmt;
   ConvFn3 fn;
-  char name[96];
+  char name[112];
 };
 
-#define HFG3_ENTRY(KT, TILE, UPS, NP) \
-  { KT, TILE, UPS, NP, Inst3<KT, TILE, UPS, NP>::fn(), {0} }
-#define HFG3_TILES(KT, UPS)                                                                  \
-  HFG3_ENTRY(KT, 0, UPS, 3), HFG3_ENTRY(KT, 1, UPS, 3), HFG3_ENTRY(KT, 2, UPS, 3),           \
-      HFG3_ENTRY(KT, 3, UPS, 3), HFG3_ENTRY(KT, 4, UPS, 3), HFG3_ENTRY(KT, 1, UPS, 2),       \
-      HFG3_ENTRY(KT, 2, UPS, 2), HFG3_ENTRY(KT, 3, UPS, 2), HFG3_ENTRY(KT, 4, UPS, 2)
+#define HFG3_ENTRY(KT, TILE, UPS, NP, FMT) \
+  { KT, TILE, UPS, NP, FMT, Inst3<KT, TILE, UPS, NP, FMT>::fn(), {0} }
+// per tile: bf16x3 (NP 3, bf16), f16x3 (NP 3, f16) and bf16w (NP 2 on the f16 kernels: the
+// bf16-rounded weights are exact f16 halves after their power-of-two scale, lo(w) = 0)
+#define HFG3_VARIANTS(KT, TILE, UPS) \
+  HFG3_ENTRY(KT, TILE, UPS, 3, 0), HFG3_ENTRY(KT, TILE, UPS, 3, 1), HFG3_ENTRY(KT, TILE, UPS, 2, 1)
+// tiles 1-4 (tile 0, the 8-wave 128x256 tile with a 3-deep slab ring, was removed in round 4:
+// slower than tile 3 / 5 everywhere it applied)
+#define HFG3_TILES(KT, UPS)                                                            \
+  HFG3_VARIANTS(KT, 1, UPS), HFG3_VARIANTS(KT, 2, UPS), HFG3_VARIANTS(KT, 3, UPS),     \
+      HFG3_VARIANTS(KT, 4, UPS)
 
-// NP 3: hi*hi + hi*lo + lo*hi (bf16x3); NP 2: hi*hi + hi*lo for bf16-valued weights
-// (HFG_DTYPE_BF16W: the weights' lo plane is zero), tiles 1-4
 // tile 5 (AREG): compile-time taps, layer convs only
-#define HFG3_AREG(KT) HFG3_ENTRY(KT, 5, false, 3), HFG3_ENTRY(KT, 5, false, 2)
+#define HFG3_AREG(KT) HFG3_VARIANTS(KT, 5, false)
 Entry3 g_entries3[] = {
     HFG3_TILES(3, false), HFG3_TILES(5, false), HFG3_TILES(7, false), HFG3_TILES(11, false),
     HFG3_TILES(0, false), HFG3_TILES(2, true),  HFG3_TILES(0, true),
@@ -788,13 +815,13 @@ size_t bf16x3_lds_bytes(int tile, int kt, int dil) {
   return sizeof(__bf16) * (t.WD * slab + 2 * 2 * xplane);  // weight ring + 2 (hi,lo) windows
 }
 
-hipError_t launch_conv_bf16x3(int tile, int kt, bool ups, int np, const ConvParams& p,
+hipError_t launch_conv_bf16x3(int tile, int kt, bool ups, int fmt, int np, const ConvParams& p,
                               int n_tiles, int m_tiles, int batch, hipStream_t stream,
                               const char** name) {
   Entry3* e = nullptr;
   Entry3* generic = nullptr;
   for (auto& cand : g_entries3) {
-    if (cand.tile != tile || cand.ups != ups || cand.np != np) continue;
+    if (cand.tile != tile || cand.ups != ups || cand.np != np || cand.fmt != fmt) continue;
     if (cand.kt == kt) e = &cand;
     if (cand.kt == 0) generic = &cand;
   }
@@ -806,9 +833,9 @@ hipError_t launch_conv_bf16x3(int tile, int kt, bool ups, int np, const ConvPara
   {
     std::lock_guard<std::mutex> lk(setup_mutex());
     if (!e->name[0])
-      snprintf(e->name, sizeof(e->name), "conv1d_bf16x3<%d, %d, %d, %d, %d, %d, %d, %s, %d%s>",
+      snprintf(e->name, sizeof(e->name), "conv1d_bf16x3<%d, %d, %d, %d, %d, %d, %d, %s, %d, %s, %d>",
                e->kt, t.TPC, t.WAVES_M, t.WAVES_N, t.WM, t.WN, t.WD, e->ups ? "true" : "false",
-               e->np, t.AREG ? ", true" : "");
+               e->np, t.AREG ? "true" : "false", e->fmt);
   }
   size_t lds = bf16x3_lds_bytes(tile, kt, p.dil);
   if (p.epi_lds && !ups)

@@ -202,6 +202,7 @@ conv1d_mfma_f32(const ConvParams p) {
 
   // ---- epilogue ----
   if constexpr (UPS) {
+    float vmax = 0.f;  // max |stored value| (f16x3 consumers: p.amax_out)
 #pragma unroll
     for (int i = 0; i < WM; ++i) {
       float bv[16];  // batch the bias loads ahead of the scattered stores
@@ -220,10 +221,14 @@ conv1d_mfma_f32(const ConvParams p) {
           const int co = row / p.ups_s;
           const int ph = row - co * p.ups_s;
           const int t = n * p.ups_s + ph - p.ups_p;
-          if (t >= 0 && t < L_out_b) p.y[(int64_t)b * p.y_bs + (int64_t)co * p.L_out + t] = v;
+          if (t >= 0 && t < L_out_b) {
+            p.y[(int64_t)b * p.y_bs + (int64_t)co * p.L_out + t] = v;
+            vmax = fmaxf(vmax, fabsf(v));
+          }
         }
       }
     }
+    if (p.amax_out) amax_commit(vmax, p.amax_out, b);
   } else if (p.epi_lds && (p.N & 3) == 0) {
     // LDS-staged float4 epilogue (epilogue.h; the host sized the LDS for it)
     // every wave is done with the main loop's LDS and no weight LDS-DMA is in flight
@@ -487,6 +492,7 @@ __global__ void __launch_bounds__(256) mrf_combine_kernel(MrfCombineArgs a) {
   const int len_b = a.len ? min(a.len[b], a.L) : a.L;
   const int64_t base = (int64_t)b * a.C * a.L;
   const int64_t n = (int64_t)a.C * a.L;
+  float vmax = 0.f;  // max |stored value| (f16x3 consumers: a.amax_out)
   for (int64_t i = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4; i < n;
        i += (int64_t)gridDim.x * 256 * 4) {
     const int t = (int)(i % a.L);
@@ -506,6 +512,7 @@ __global__ void __launch_bounds__(256) mrf_combine_kernel(MrfCombineArgs a) {
       acc.z = acc.z / a.div;
       acc.w = acc.w / a.div;
       *reinterpret_cast<float4*>(a.y + base + i) = acc;
+      vmax = fmaxf(vmax, fmaxf(fmaxf(fabsf(acc.x), fabsf(acc.y)), fmaxf(fabsf(acc.z), fabsf(acc.w))));
     } else {
       // a group of 4 can straddle two channel rows: each sample tests its own column
       // (skipping the group on its first sample's column lost the next row's first
@@ -515,9 +522,11 @@ __global__ void __launch_bounds__(256) mrf_combine_kernel(MrfCombineArgs a) {
         float acc = a.o[0][base + i + e];
         for (int j = 1; j < a.n; ++j) acc = acc + a.o[j][base + i + e];
         a.y[base + i + e] = acc / a.div;
+        vmax = fmaxf(vmax, fabsf(acc / a.div));
       }
     }
   }
+  if (a.amax_out) amax_commit(vmax, a.amax_out, b);
 }
 
 hipError_t launch_mrf_combine(const MrfCombineArgs& a, int batch, hipStream_t stream) {
@@ -525,6 +534,33 @@ hipError_t launch_mrf_combine(const MrfCombineArgs& a, int batch, hipStream_t st
   const int64_t n4 = ((int64_t)a.C * a.L + 3) / 4;
   const int gx = (int)std::min<int64_t>((n4 + 255) / 256, 4096);
   mrf_combine_kernel<<<dim3(gx, batch), dim3(256), 0, stream>>>(a);
+  return hipGetLastError();
+}
+
+// max |x| per item over its valid columns, folded into out[b] (one atomic per wave)
+__global__ void __launch_bounds__(256)
+absmax_kernel(const float* __restrict__ x, int64_t x_bs, int64_t x_cs, int64_t x_ts, int C, int L,
+              const int32_t* __restrict__ len, uint32_t* __restrict__ out) {
+  const int b = blockIdx.y;
+  const int len_b = len ? min(max(len[b], 0), L) : L;
+  const float* xb = x + (int64_t)b * x_bs;
+  const int64_t n = (int64_t)C * len_b;
+  float m = 0.f;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    // element i of the item in (time-major for x_ts == 1 ? channel-major) order
+    const int64_t c = x_ts == 1 ? i / len_b : i % C;
+    const int64_t t = x_ts == 1 ? i % len_b : i / C;
+    m = fmaxf(m, fabsf(xb[c * x_cs + t * x_ts]));
+  }
+  amax_commit(m, out, b);
+}
+
+hipError_t launch_absmax(const float* x, int64_t x_bs, int64_t x_cs, int64_t x_ts, int C, int L,
+                         const int32_t* len, int batch, uint32_t* out, hipStream_t stream) {
+  const int64_t n = (int64_t)C * L;
+  const int gx = (int)std::min<int64_t>((n + 256 * 16 - 1) / (256 * 16), 1024);
+  absmax_kernel<<<dim3(gx > 0 ? gx : 1, batch), dim3(256), 0, stream>>>(x, x_bs, x_cs, x_ts, C, L,
+                                                                       len, out);
   return hipGetLastError();
 }
 

@@ -17,6 +17,25 @@ namespace hfg {
 
 typedef float floatx16e __attribute__((ext_vector_type(16)));
 
+// largest value over a wave's lanes
+__device__ __forceinline__ float wave_max(float m) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+  return m;
+}
+// fold a lane's max |value| into item b's producer slot: one vector atomic per wave (the
+// slots are zeroed by the host before the forward; non-negative floats order like their bit
+// patterns).  An item's slot is kAmaxSpread words and each wave updates the one its block
+// and wave index select, so same-address atomics do not serialise a whole grid; the
+// consumer takes the max of the kAmaxSpread words (x3_exp_slot).
+__device__ __forceinline__ void amax_commit(float m, uint32_t* slots, int b) {
+  m = wave_max(m);
+  const unsigned blk = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+  const unsigned w = blk * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  uint32_t* slot = slots + (size_t)b * kAmaxSpread + (w & (kAmaxSpread - 1));
+  if ((threadIdx.x & 63) == 0) atomicMax(slot, __builtin_bit_cast(uint32_t, m));
+}
+
 template <int WM, int WN>
 __device__ __forceinline__ void conv_epilogue(const ConvParams& p, const float* __restrict__ bias,
                                               floatx16e (&acc)[WM][WN], int b, int row_base,
@@ -31,6 +50,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvParams& p, const float* 
   // without per-element exec-mask branches
   const int row_u = __builtin_amdgcn_readfirstlane(row_base);
   const int n_u = __builtin_amdgcn_readfirstlane(n_base);
+  float vmax = 0.f;  // max |stored value| (f16x3 consumers: p.amax_out)
   // bias: padded to the m-tile, every row index is readable
 #pragma unroll
   for (int i = 0; i < WM; ++i) {
@@ -74,6 +94,10 @@ __device__ __forceinline__ void conv_epilogue(const ConvParams& p, const float* 
 #pragma unroll
         for (int r = 0; r < 16; ++r) v[r] = v[r] / p.mrf_div;
       }
+      if (p.amax_out) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) vmax = ok[r] ? fmaxf(vmax, fabsf(v[r])) : vmax;
+      }
       if (n_u + k * 32 + 31 < N_b && row_u + i * 32 + 31 < p.M) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) *reinterpret_cast<float*>(outb + off[r]) = v[r];
@@ -84,6 +108,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvParams& p, const float* 
       }
     }
   }
+  if (p.amax_out) amax_commit(vmax, p.amax_out, b);
 }
 
 template <int WM, int WN>
@@ -113,6 +138,7 @@ __device__ __forceinline__ void conv_epilogue_lds(const ConvParams& p, floatx16e
   const bool add_mrf = p.mrf && (p.mrf_mode & 1);
   const bool div_mrf = p.mrf && (p.mrf_mode & 2);
   const bool act = p.act_out != 0;
+  float vmax = 0.f;  // max |stored value| (f16x3 consumers: p.amax_out)
 #pragma unroll
   for (int i = 0; i < WM; ++i) {
 #pragma unroll
@@ -205,6 +231,17 @@ __device__ __forceinline__ void conv_epilogue_lds(const ConvParams& p, floatx16e
           v[u].w = v[u].w / p.mrf_div;
         }
       }
+      if (p.amax_out) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          // the stored elements only: a partial quad's tail past N_b is not written
+          const int nv = ok[u] ? min(N_b - n[u], 4) : 0;
+          vmax = nv > 0 ? fmaxf(vmax, fabsf(v[u].x)) : vmax;
+          vmax = nv > 1 ? fmaxf(vmax, fabsf(v[u].y)) : vmax;
+          vmax = nv > 2 ? fmaxf(vmax, fabsf(v[u].z)) : vmax;
+          vmax = nv > 3 ? fmaxf(vmax, fabsf(v[u].w)) : vmax;
+        }
+      }
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         float* dst = outb + (int64_t)row[u] * p.N + n[u];
@@ -222,6 +259,7 @@ __device__ __forceinline__ void conv_epilogue_lds(const ConvParams& p, floatx16e
     }
     __builtin_amdgcn_wave_barrier();
   }
+  if (p.amax_out) amax_commit(vmax, p.amax_out, b);
 }
 
 }  // namespace hfg

@@ -75,7 +75,8 @@ struct Layer {
   int s, p;          // ConvTranspose1d stride / padding
   // GEMM view
   int M, KT, CK, tile, m_tiles, n_chunks;
-  int prec;          // 0: fp32 MFMA kernel, 1: bf16x3 split-precision kernel
+  int prec;          // 0: fp32 MFMA kernel, 1: split-precision kernel (bf16x3 / f16x3)
+  int ew = 0;        // f16x3: power-of-two exponent of this layer's weight packing
   size_t w_off, b_off;  // offsets (floats) into the packed device buffer
   size_t w_len, b_len;
   // bf16x3 layers: a second packing for the small-grid tile (kBf16x3SmallTile), -1: none
@@ -87,8 +88,15 @@ struct Layer {
   size_t wf_off = 0, bf_off = 0;
 };
 
-// bf16x3 and bf16w both run the split-operand bf16 MFMA kernels
-inline bool split_dtype(int dtype) { return dtype == HFG_DTYPE_BF16X3 || dtype == HFG_DTYPE_BF16W; }
+// f16x3, bf16x3 and bf16w run the split-operand MFMA kernels (f16x3 and bf16w in the f16
+// format with power-of-two scales, bf16x3 in the bf16 format: bf16x3_common.h)
+inline bool split_dtype(int dtype) {
+  return dtype == HFG_DTYPE_F16X3 || dtype == HFG_DTYPE_BF16X3 || dtype == HFG_DTYPE_BF16W;
+}
+// (the exact-fp32 mode has no split format: -1, no scale slots)
+inline int split_fmt(int dtype) {
+  return dtype == HFG_DTYPE_BF16X3 ? hfg::kFmtBf16 : split_dtype(dtype) ? hfg::kFmtF16 : -1;
+}
 
 struct Param {
   std::vector<int64_t> shape;
@@ -160,38 +168,23 @@ struct hfg_handle {
   void* ws = nullptr;
   size_t ws_bytes = 0;
   bool profiling = false;
-  int big_tile = 3;  // bf16x3 tile for M >= 128 (HFG_BF16X3_BIGTILE env: 0 or 3)
-  bool use_fused_rb = true;
-  bool rb64_narrow = true;   // 256-column whole-ResBlock window for C = 64, k = 3 (HFG_RB64_NARROW=0 disables)  // whole-ResBlock kernel for C in {32, 64} (HFG_FUSED_RB=0 disables)
+  bool use_fused_rb = true;  // whole-ResBlock kernel for C in {32, 64, 128} (HFG_FUSED_RB=0:
+                             // layer by layer; the parity suites compare both schedules)
   bool rb_split = true;      // whole-ResBlock split in two launches where it cuts >= 10 % of the
-                             // halo recompute (k = 11 in V1; HFG_RB_SPLIT=0: off)
-  double rb_split_min = 0.9; // split when its MFMA work <= this x one launch's (HFG_RB_SPLIT_MIN)
-  int rb_waves_n32 = 4;      // window of the C = 32 ResBlock kernel: 128 * this columns
-                             // (HFG_RB_WN32: 4 or 8)
-  int ups_swizzle = 1;       // XCD swizzle of the upsampler blocks (HFG_UPS_SWIZZLE=0: off)
-  int ups_small_rows = 0;    // output-frame upsamplers of at most this many rows per class on
-                             // the 32-row tile (HFG_UPS_SMALL_ROWS)
-  bool post4 = true;         // conv_post on the 4-samples-per-thread kernel where L % 4 == 0
-                             // (HFG_POST4=0: the LDS-staged kernel; bitwise the same wav)
+                             // halo recompute (k = 11 in V1; HFG_RB_SPLIT=0: one launch)
   int ups_frames = 1;        // k = 2u upsamplers on the output-frame kernel: 1 when its grid
-                             // fills the chip, 2 always, 0 never (HFG_UPS_FRAMES; the
-                             // polyphase conv1d_bf16x3 path gives the bitwise same result)
-  int np = 3;                // MFMA products per multiply-add: 3 (bf16x3), 2 (bf16w: lo(w) = 0)
-  int areg = 1;              // tile-3 layer convs on tile 5 (A in registers; HFG_AREG=0: off)
-  int epi_lds = 1;           // LDS-staged float4 epilogue of the bf16x3 layer convs (HFG_EPI_LDS=0: off)
+                             // fills the chip, 2 always (HFG_UPS_FRAMES; the polyphase
+                             // conv1d_bf16x3 path gives the bitwise same result)
+  int fmt = 0;               // split format of the split kernels (bf16x3_common.h)
+  int np = 3;                // MFMA products per multiply-add: 3, or 2 (bf16w: lo(w) = 0)
   int small_tile = -1;       // small-grid tile: -1 auto (grid < kSmallGridBlocks), 0 never,
-                             // 1 always (HFG_SMALL_TILE)
-  int thin_mfma = -1;        // bf16x3 thin stages on mrf_thin_mfma: -1 auto (C = 16; the
-                             // C = 8 stage stays on the VALU kernel), 0 none, 1 every C
-                             // (HFG_THIN_MFMA)
-  bool thin = true;          // whole-MRF VALU kernel for C <= 16 stages (HFG_THIN=0: layer
-                             // kernels instead)
-  int dbg_flags = 0;  // HFG_DEBUG_FLAGS env (kernel ablations; wrong results when set)
+                             // 1 always (HFG_SMALL_TILE; bitwise invisible)
+  int dbg_flags = 0;  // HFG_DEBUG_FLAGS (kernel ablations, -DHFG_ABLATE=1 builds only)
   // batch split over two HIP streams (HFG_SPLIT=1 disables): the two halves' launches
   // overlap, so one half's ramp-down / epilogue tail runs beside the other's main loops
   int split = 2;
-  int64_t split_min_frames = 4096;  // batch frames from which a forward runs as two halves
-                                    // on two streams (HFG_SPLIT_MIN)
+  static constexpr int64_t kSplitMinFrames = 4096;  // batch frames from which a forward runs as
+                                                    // two halves on two streams
   hipStream_t aux = nullptr;
   hipEvent_t fork_ev = nullptr, join_ev = nullptr;
   // concurrent ResBlocks of small forwards (HFG_RB_CONC: -1 auto, 0 off, 1 whenever the
@@ -226,9 +219,9 @@ int validate_config(const hfg_config* c) {
   if (c->n_mels <= 0) return fail(HFG_EINVAL, "n_mels must be > 0");
   if (c->n_up <= 0 || c->n_up > HFG_MAX_STAGES) return fail(HFG_EINVAL, "n_up out of range");
   if (c->n_res <= 0 || c->n_res > HFG_MAX_RES) return fail(HFG_EINVAL, "n_res out of range");
-  if (c->dtype != HFG_DTYPE_FP32 && c->dtype != HFG_DTYPE_BF16X3 && c->dtype != HFG_DTYPE_BF16W)
-    return fail(HFG_EINVAL,
-                "dtype must be HFG_DTYPE_FP32 (0), HFG_DTYPE_BF16X3 (1) or HFG_DTYPE_BF16W (2)");
+  if (c->dtype != HFG_DTYPE_FP32 && !split_dtype(c->dtype))
+    return fail(HFG_EINVAL, "dtype must be HFG_DTYPE_FP32 (0), HFG_DTYPE_BF16X3 (1), "
+                "HFG_DTYPE_BF16W (2) or HFG_DTYPE_F16X3 (3)");
   if (c->c0 <= 0) return fail(HFG_EINVAL, "upsample_initial_channel must be > 0");
   for (int i = 0; i < c->n_up; ++i) {
     if (c->up_rates[i] <= 0 || c->up_kernels[i] <= 0)
@@ -353,10 +346,10 @@ int build_layers(hfg_handle* h) {
     if (split_dtype(h->cfg.dtype) && (L.kind == L_CONV || L.kind == L_UPS) &&
         hfg::bf16x3_tile_for_rows(L.M) >= 0 && hfg::bf16x3_supported(L.KT, L.dil)) {
       // split-precision path: chunk = 16 channels x TPC taps
-      L.tile = hfg::bf16x3_tile_for_rows(L.M, h->big_tile);
+      L.tile = hfg::bf16x3_tile_for_rows(L.M);
       // tile 3 with the A fragments in registers (same packing): layer convs whose tap
       // count has a compile-time instance, whole 16-channel groups
-      if (h->areg && L.tile == 3 && L.kind == L_CONV && L.C_in % 16 == 0 &&
+      if (L.tile == 3 && L.kind == L_CONV && L.C_in % 16 == 0 &&
           (L.KT == 3 || L.KT == 5 || L.KT == 7 || L.KT == 11))
         L.tile = hfg::kAregTile;
       const hfg::Bf16x3Cfg& t3 = hfg::kBf16x3Tiles[L.tile];
@@ -386,10 +379,10 @@ int build_layers(hfg_handle* h) {
       const int rows_f = L.kind == L_UPS ? L.C_out * L.s / 2 : 0;
       if (L.kind == L_UPS && h->ups_frames && L.k == 2 * L.s && hfg::ups_rate_ok(L.s) &&
           L.p == L.s / 2 && L.C_in % 16 == 0) {
-        // the 32-row tile (3 waves per SIMD) where the 64-row one does not divide the rows,
-        // or up to HFG_UPS_SMALL_ROWS rows
+        // the 32-row tile (3 waves per SIMD) where the 64-row one does not divide the rows
+        // (running more stages on it measured slower: two m-tiles stage one window twice)
         const bool small = rows_f % hfg::kUpsCfgs[1].MT() == 0 &&
-                           (rows_f % hfg::kUpsCfgs[0].MT() != 0 || rows_f <= h->ups_small_rows);
+                           rows_f % hfg::kUpsCfgs[0].MT() != 0;
         const int cfg = small                                 ? 1
                         : rows_f % hfg::kUpsCfgs[0].MT() == 0 ? 0
                                                                : -1;
@@ -437,9 +430,7 @@ int build_layers(hfg_handle* h) {
       rb.kt = c.res_kernels[j];
       // C = 64, k = 3: a 256-column window (5 % more halo recompute than 512) whose small
       // LDS footprint lets two blocks share a CU and overlap their operand rewrites
-      const int waves_n = C == 128 ? 2
-                          : C == 64  ? (rb.kt == 3 && h->rb64_narrow ? 2 : 4)
-                                     : h->rb_waves_n32;
+      const int waves_n = C == 128 ? 2 : C == 64 ? (rb.kt == 3 ? 2 : 4) : 4;
       const int nwin = hfg::kRbColsPerWave * waves_n;
       rb.waves_n = waves_n;
       bool ok = rb.kt % 2 == 1 && hfg::rb_supported(C, rb.kt, waves_n) &&
@@ -483,7 +474,7 @@ int build_layers(hfg_handle* h) {
             rb.W_p[1] = w1;
           }
         }
-        if (best > h->rb_split_min * whole) rb.split = 0;
+        if (best > 0.9 * whole) rb.split = 0;
       }
       rb.w_off = off;
       rb.w_len = (size_t)rb.convs.size() * C * C * rb.kt;  // bf16 hi + lo = one float each
@@ -498,7 +489,7 @@ int build_layers(hfg_handle* h) {
   for (auto& st : h->stages) {
     const int C = st.C;
     const int nwin = hfg::thin_window(C);
-    if (!h->thin || nwin == 0 || c.n_res > hfg::kThinMaxRes) continue;
+    if (nwin == 0 || c.n_res > hfg::kThinMaxRes) continue;
     int n_conv = 0, halo_max = 0;
     bool ok = true;
     std::vector<int> convs, conv0, halos;
@@ -534,8 +525,7 @@ int build_layers(hfg_handle* h) {
     // bf16x3: the MFMA variant when every conv's zero-padded last k-step stays in the
     // operand margin
     const int tps = 32 / C;
-    bool mf = split_dtype(h->cfg.dtype) && h->thin_mfma != 0 &&
-              (h->thin_mfma == 1 || C == 16) && hfg::thin_mfma_window(C) > 0 &&
+    bool mf = split_dtype(h->cfg.dtype) && C == 16 && hfg::thin_mfma_window(C) > 0 &&
               hfg::thin_mfma_window(C) - 2 * halo_max >= hfg::thin_mfma_window(C) / 4;
     size_t bytes = 0;
     st.thin_m_conv.clear();
@@ -573,6 +563,44 @@ inline float bf2f(uint16_t b) {
   memcpy(&f, &u, 4);
   return f;
 }
+// float -> f16 bits, round to nearest even (subnormals kept)
+inline uint16_t f2h(float f) {
+  const _Float16 h = (_Float16)f;
+  uint16_t u;
+  memcpy(&u, &h, 2);
+  return u;
+}
+inline float h2f(uint16_t u) {
+  _Float16 h;
+  memcpy(&h, &u, 2);
+  return (float)h;
+}
+// f16x3 exponent of a tensor with max |value| m: m 2^e in [2^14, 2^15), clamped like the
+// device's x3_exp (bf16x3_common.h)
+int x3_exp_host(float m) {
+  if (!(m > 0.f) || !std::isfinite(m)) return 0;
+  int x = 0;
+  std::frexp(m, &x);
+  return std::min(std::max(15 - x, -hfg::kX3ExpMax), hfg::kX3ExpMax);
+}
+// how one layer's weights are split into the kernels' (hi, lo) planes
+struct WSplit {
+  int fmt;      // hfg::kFmtBf16 / kFmtF16
+  float scale;  // 2^ew (f16)
+};
+inline WSplit wsplit(const hfg_handle* h, const Layer& L) {
+  return WSplit{h->fmt, std::ldexp(1.0f, L.ew)};
+}
+inline void split_w(float v, const WSplit& ws, uint16_t& hi, uint16_t& lo) {
+  if (ws.fmt == hfg::kFmtBf16) {
+    hi = f2bf(v);
+    lo = f2bf(v - bf2f(hi));
+  } else {
+    const float a = v * ws.scale;  // exact (power of two)
+    hi = f2h(a);
+    lo = f2h(a - h2f(hi));
+  }
+}
 
 // mrf_thin weights: per conv [tap][ci][co] fp32 (the C output channels of one (tap, ci)
 // are one scalar load), biases [conv][C]
@@ -590,14 +618,13 @@ void pack_thin(hfg_handle* h, const Stage& st) {
     for (int co = 0; co < C; ++co) h->packed_host[st.thin_b_off + e * C + co] = bsrc[co];
   }
   if (!st.thin_mfma) return;
-  // mrf_thin_mfma A stream: per (conv, k-step) [plane][lane][8] bf16, lane l -> row
-  // r = l & 15, K = 8 * (l >> 4) + e.  C = 16: plane 0 = hi, 1 = lo of w[r][ci][tap],
-  // ci = 8 ((l >> 4) & 1) + e, tap = 2 s + (l >> 5).  C = 8: ci = e, tap = 4 s + (l >> 4);
-  // plane 0 = [hi; lo] (rows 8-15 = lo of row - 8), plane 1 = [hi; 0].
+  // mrf_thin_mfma A stream (C = 16): per (conv, k-step) [plane][lane][8], lane l -> row
+  // r = l & 15, ci = 8 ((l >> 4) & 1) + e, tap = 2 s + (l >> 5); plane 0 = hi, 1 = lo
   uint16_t* dst = reinterpret_cast<uint16_t*>(h->packed_host.data() + st.thin_m_off);
   const int tps = 32 / C;
   for (size_t e = 0; e < st.thin_convs.size(); ++e) {
     const Layer& L = h->layers[st.thin_convs[e]];
+    const WSplit ws = wsplit(h, L);
     const float* w = h->params[L.mod + ".weight"].data.data();  // [C_out][C_in][k]
     const int steps = (L.k + tps - 1) / tps;
     uint16_t* de = dst + st.thin_m_conv[e] / 2;
@@ -605,26 +632,12 @@ void pack_thin(hfg_handle* h, const Stage& st) {
       for (int plane = 0; plane < 2; ++plane)
         for (int lane = 0; lane < 64; ++lane)
           for (int el = 0; el < 8; ++el) {
-            const int r = lane & 15, qq = lane >> 4;
-            int co, ci, tap;
-            bool lo_row = false;
-            if (C == 16) {
-              co = r;
-              ci = 8 * (qq & 1) + el;
-              tap = 2 * s + (qq >> 1);
-            } else {
-              co = r & 7;
-              lo_row = r >= 8;
-              ci = el;
-              tap = 4 * s + qq;
-            }
+            const int co = lane & 15, qq = lane >> 4;
+            const int ci = 8 * (qq & 1) + el, tap = 2 * s + (qq >> 1);
             const float v = tap < L.k ? w[((size_t)co * C + ci) * L.k + tap] : 0.f;
-            const uint16_t hi = f2bf(v);
-            const uint16_t lo = f2bf(v - bf2f(hi));
-            uint16_t out;
-            if (C == 16) out = plane == 0 ? hi : lo;
-            else out = plane == 0 ? (lo_row ? lo : hi) : (lo_row ? (uint16_t)0 : hi);
-            de[((size_t)(s * 2 + plane) * 64 + lane) * 8 + el] = out;
+            uint16_t hi, lo;
+            split_w(v, ws, hi, lo);
+            de[((size_t)(s * 2 + plane) * 64 + lane) * 8 + el] = plane == 0 ? hi : lo;
           }
   }
 }
@@ -658,7 +671,7 @@ void pack_gemm_weights(const Layer& L, F wt, float* dst) {
 //   row = mt*MT + wave_m*32*WM + wm*32 + (lane & 31), ci = g*16 + 8*(lane >> 5) + e,
 //   tap = tg*TPC + jj; plane 0 = bf16(w), plane 1 = bf16(w - hi).
 template <typename F>
-void pack_bf16x3(const Layer& L, F wt, uint16_t* dst) {
+void pack_bf16x3(const Layer& L, F wt, const WSplit& ws, uint16_t* dst) {
   const hfg::Bf16x3Cfg& t = hfg::kBf16x3Tiles[L.tile];
   const int TPC = t.TPC;
   const int n_g = (L.C_in + 15) / 16, n_tg = (L.KT + TPC - 1) / TPC;
@@ -677,8 +690,9 @@ void pack_bf16x3(const Layer& L, F wt, uint16_t* dst) {
                     const int tap = tg * TPC + jj;
                     float v = 0.f;
                     if (row < L.M && ci < L.C_in && tap < L.KT) v = wt(row, ci, tap);
-                    const uint16_t hi = f2bf(v);
-                    dst[idx++] = plane == 0 ? hi : f2bf(v - bf2f(hi));
+                    uint16_t hi, lo;
+                    split_w(v, ws, hi, lo);
+                    dst[idx++] = plane == 0 ? hi : lo;
                   }
 }
 
@@ -697,6 +711,7 @@ void pack_resblock(hfg_handle* h, const RbFused& rb) {
   for (int wm = 0; wm < C / 32; ++wm)
     for (int e = 0; e < n_conv; ++e) {
       const Layer& L = h->layers[rb.convs[e]];
+      const WSplit ws = wsplit(h, L);
       const float* w = h->params[L.mod + ".weight"].data.data();  // [C_out][C_in][k]
       for (int g = 0; g < n_g; ++g)
         for (int tap = 0; tap < KT; ++tap)
@@ -706,8 +721,9 @@ void pack_resblock(hfg_handle* h, const RbFused& rb) {
                 const int row = wm * 32 + (lane & 31);
                 const int ci = g * 16 + 4 * (lane >> 5) + (el & 3) + 8 * (el >> 2);
                 const float v = w[((size_t)row * C + ci) * KT + tap];
-                const uint16_t hi = f2bf(v);
-                dst[idx++] = plane == 0 ? hi : f2bf(v - bf2f(hi));
+                uint16_t hi, lo;
+                split_w(v, ws, hi, lo);
+                dst[idx++] = plane == 0 ? hi : lo;
               }
     }
   for (int e = 0; e < n_conv; ++e) {
@@ -728,6 +744,7 @@ void pack_ups_frames(hfg_handle* h, const Layer& L) {
   const float* w = h->params[L.mod + ".weight"].data.data();
   const float* bias = h->params[L.mod + ".bias"].data.data();
   uint16_t* dst = reinterpret_cast<uint16_t*>(h->packed_host.data() + L.wf_off);
+  const WSplit ws = wsplit(h, L);
   const int u = L.s, hh = u / 2, k = L.k, cout = L.C_out, n_g = L.C_in / 16;
   size_t idx = 0;
   for (int mt = 0; mt < L.m_tiles_f; ++mt)
@@ -744,8 +761,9 @@ void pack_ups_frames(hfg_handle* h, const Layer& L) {
                     const int ci = g * 16 + 8 * (lane >> 5) + e;
                     const int j = c == 0 ? (tp == 0 ? sp + hh + u : sp + hh) : (tp == 0 ? sp + u : sp);
                     const float v = w[((size_t)ci * cout + co) * k + j];
-                    const uint16_t hi = f2bf(v);
-                    dst[idx++] = plane == 0 ? hi : f2bf(v - bf2f(hi));
+                    uint16_t hi, lo;
+                    split_w(v, ws, hi, lo);
+                    dst[idx++] = plane == 0 ? hi : lo;
                   }
   float* bdst = h->packed_host.data() + L.bf_off;
   for (int co = 0; co < cout; ++co) bdst[co] = bias[co];
@@ -779,7 +797,7 @@ void pack_layer(hfg_handle* h, const Layer& L) {
       if (L.kind == L_CONV) {
         const int cin = L.C_in, k = L.k;
         pack_bf16x3(Lp, [&](int row, int ci, int j) { return w[((size_t)row * cin + ci) * k + j]; },
-                    reinterpret_cast<uint16_t*>(wd));
+                    wsplit(h, L), reinterpret_cast<uint16_t*>(wd));
         for (size_t m = 0; m < Lp.b_len; ++m) bd[m] = m < (size_t)L.M ? Bp.data[m] : 0.f;
       } else {
         const int s = L.s, Q = L.KT, k = L.k, cout = L.C_out;
@@ -789,7 +807,7 @@ void pack_layer(hfg_handle* h, const Layer& L) {
                       const int kidx = r + s * (Q - 1 - jj);
                       return kidx < k ? w[((size_t)ci * cout + co) * k + kidx] : 0.f;
                     },
-                    reinterpret_cast<uint16_t*>(wd));
+                    wsplit(h, L), reinterpret_cast<uint16_t*>(wd));
         for (size_t m = 0; m < Lp.b_len; ++m) bd[m] = m < (size_t)L.M ? Bp.data[m / s] : 0.f;
       }
     }
@@ -833,6 +851,14 @@ int do_commit(hfg_handle* h) {
     }
   }
   std::fill(h->packed_host.begin(), h->packed_host.end(), 0.f);
+  // f16x3 weight scales: one power of two per layer, from its largest |weight|
+  for (auto& L : h->layers) {
+    L.ew = 0;
+    if (h->fmt != hfg::kFmtF16 || L.kind == L_POST) continue;
+    float m = 0.f;
+    for (float v : h->params[L.mod + ".weight"].data) m = std::max(m, std::fabs(v));
+    L.ew = x3_exp_host(m);
+  }
   for (auto& L : h->layers) pack_layer(h, L);
   for (auto& st : h->stages) {
     for (auto& rb : st.rbs)
@@ -909,17 +935,25 @@ bool any_conc(const hfg_handle* h, int64_t B, int64_t T) {
 int n_bufs(const hfg_handle* h, int64_t B, int64_t T, bool conc_ok) {
   return 4 + (conc_ok && any_conc(h, B, T) ? 3 * h->cfg.n_res : 0);
 }
+// f16x3 scale slots of one forward part: one [B] row of per-item max |value| per producing
+// launch (the mel's absmax, conv_pre, every upsampler, layer conv and MRF output), zeroed at
+// the start of the forward
+int n_slots(const hfg_handle* h) { return (int)h->layers.size() + 2 * h->cfg.n_up + 4; }
+size_t slots_bytes(const hfg_handle* h, int64_t B) {
+  if (h->fmt != hfg::kFmtF16) return 0;
+  return ((size_t)n_slots(h) * (size_t)B * hfg::kAmaxSpread * sizeof(uint32_t) + 255) & ~(size_t)255;
+}
 // workspace of one forward_impl call (one batch half)
 size_t ws_part_bytes(const hfg_handle* h, int64_t B, int64_t T, bool conc_ok = false) {
   const size_t n = (size_t)n_bufs(h, B, T, conc_ok) * sizeof(float) *
                        (size_t)shapes_for(h, B, T).buf_elems +
-                   lens_table_bytes(h, B);
+                   lens_table_bytes(h, B) + slots_bytes(h, B);
   return (n + 255) & ~(size_t)255;
 }
 // small forwards stay on one stream: splitting them doubles an already latency-bound
 // launch count (measured: 32 x 62 frames 5.4 -> 5.6 ms split)
 bool split_batch(const hfg_handle* h, int64_t B, int64_t T) {
-  return h->split >= 2 && B >= 2 && B * T >= h->split_min_frames;
+  return h->split >= 2 && B >= 2 && B * T >= hfg_handle::kSplitMinFrames;
 }
 // workspace of a forward: both halves' when the batch is split over two streams (whose
 // ResBlocks then run one after another), else one part with concurrent ResBlocks allowed
@@ -948,13 +982,32 @@ void recycle_prof(hfg_handle* h) {
   h->prof.clear();
 }
 
+// f16x3 activation scales of one forward part (bf16x3_common.h): slot rows handed out in
+// launch order; base null in the unscaled modes (every take() is then null)
+struct Slots {
+  uint32_t* base = nullptr;
+  int n = 0, next = 0;
+  int64_t B = 0;
+  uint32_t* take() {
+    if (!base) return nullptr;
+    if (next >= n) {  // sized by n_slots(): a schedule that needs more is a bug
+      overflow = true;
+      return nullptr;
+    }
+    return base + (size_t)(next++) * (size_t)B * hfg::kAmaxSpread;
+  }
+  bool overflow = false;
+};
+
 struct Launcher {
   hfg_handle* h;
   hipStream_t stream;
   int part = 0;
   int seq = 0;
   int conc = 1;  // launches of this schedule running side by side (concurrent ResBlocks)
+  Slots* sl = nullptr;
   ProfRec* rec = nullptr;
+  uint32_t* take() { return sl ? sl->take() : nullptr; }
   void begin(double flop, double bytes) {
     rec = nullptr;
     if (!h->profiling) return;
@@ -993,9 +1046,11 @@ int pick_tile(const hfg_handle* h, const Layer& L, hfg::ConvParams& p, int64_t n
 }
 
 // One conv-layer launch (regular Conv1d).
+// ain / aout: f16x3 scale slots of the input (its producer's) and of this launch's output
 int run_conv(hfg_handle* h, Launcher& ln, const Layer& L, const float* x, int64_t B, int64_t Lt,
              float* y, bool act_in, bool act_out, const float* res, float* mrf, int mrf_mode,
-             float mrf_div, const int32_t* lens, bool x_btc = false) {
+             float mrf_div, const int32_t* lens, const uint32_t* ain, uint32_t* aout,
+             bool x_btc = false) {
   ConvParams p{};
   p.x = x;
   p.x_bs = (int64_t)L.C_in * Lt;
@@ -1022,7 +1077,10 @@ int run_conv(hfg_handle* h, Launcher& ln, const Layer& L, const float* x, int64_
   p.mrf_div = mrf_div;
   p.n_chunks = L.n_chunks;
   p.dbg = h->dbg_flags;
-  p.epi_lds = h->epi_lds;
+  p.epi_lds = 1;
+  p.amax_in = ain;
+  p.amax_out = aout;
+  p.ew = L.ew;
   const int ntile = L.prec == 1 ? hfg::kBf16x3Tiles[L.tile].NTILE() : kTiles[L.tile].NTILE();
   int n_tiles = (int)((Lt + ntile - 1) / ntile), m_tiles = L.m_tiles;
   const int tile = pick_tile(h, L, p, Lt, B, ln.conc, n_tiles, m_tiles);
@@ -1033,8 +1091,8 @@ int run_conv(hfg_handle* h, Launcher& ln, const Layer& L, const float* x, int64_
   const char* name = nullptr;
   ln.begin(flop, bytes);
   hipError_t e = L.prec == 1
-                     ? hfg::launch_conv_bf16x3(tile, L.KT, false, h->np, p, n_tiles, m_tiles, (int)B,
-                                               ln.stream, &name)
+                     ? hfg::launch_conv_bf16x3(tile, L.KT, false, h->fmt, h->np, p, n_tiles, m_tiles,
+                                               (int)B, ln.stream, &name)
                      : hfg::launch_conv((TileId)L.tile, L.KT, false, p, n_tiles, L.m_tiles,
                                         (int)B, ln.stream, &name);
   ln.end(name);
@@ -1048,7 +1106,7 @@ int run_conv(hfg_handle* h, Launcher& ln, const Layer& L, const float* x, int64_
 // [split, n) read it back and do the MRF epilogue.  fp32 round trip: bitwise the same x.
 int run_resblock(hfg_handle* h, Launcher& ln, const RbFused& rb, const float* x, int64_t B,
                  int64_t Lt, float* mrf, int mrf_mode, float mrf_div, const int32_t* lens,
-                 float* scratch) {
+                 float* scratch, uint32_t* aout) {
   const Layer& L0 = h->layers[rb.convs[0]];
   const int C = L0.C_out;
   const int n_all = (int)rb.convs.size();
@@ -1072,6 +1130,7 @@ int run_resblock(hfg_handle* h, Launcher& ln, const RbFused& rb, const float* x,
     for (int e = c0; e < c1; ++e) {
       const Layer& L = h->layers[rb.convs[e]];
       p.dil[e - c0] = L.dil;
+      p.ew[e - c0] = L.ew;
       flop += 2.0 * L.C_out * L.C_in * L.k * (double)Lt * B;
     }
     p.halo = n_part == 1 ? rb.halo : rb.halo_p[part];
@@ -1080,13 +1139,14 @@ int run_resblock(hfg_handle* h, Launcher& ln, const RbFused& rb, const float* x,
     p.mrf_mode = last ? mrf_mode : 0;
     p.mrf_div = mrf_div;
     p.mrf_rcp = hfg::fast_div_ok(mrf_div) ? 1.0f / mrf_div : 0.0f;
+    p.amax_out = last ? aout : nullptr;
     p.dbg = h->dbg_flags;
     const double bytes =
         4.0 * B * Lt * C * ((last && (mrf_mode & 1)) ? 3 : 2) + 4.0 * (double)rb.w_len;
     const char* name = nullptr;
     ln.begin(flop, bytes);
     hipError_t e =
-        hfg::launch_resblock_bf16x3(C, rb.waves_n, rb.kt, h->np, p, (int)B, ln.stream, &name);
+        hfg::launch_resblock_bf16x3(C, rb.waves_n, rb.kt, h->fmt, h->np, p, (int)B, ln.stream, &name);
     ln.end(name);
     if (e != hipSuccess)
       return fail(HFG_EIO, "launch resblock %s: %s", L0.mod.c_str(), hipGetErrorString(e));
@@ -1095,7 +1155,8 @@ int run_resblock(hfg_handle* h, Launcher& ln, const RbFused& rb, const float* x,
 }
 
 int run_ups(hfg_handle* h, Launcher& ln, const Layer& L, const float* x, int64_t B, int64_t Lin,
-            int64_t Lout, float* y, const int32_t* len_in, const int32_t* len_out) {
+            int64_t Lout, float* y, const int32_t* len_in, const int32_t* len_out,
+            const uint32_t* ain, uint32_t* aout) {
   const double flop = 2.0 * L.C_in * L.C_out * L.k * (double)Lin * B;
   const double bytes = 4.0 * B * (L.C_in * Lin + L.C_out * Lout) + 4.0 * L.C_in * L.C_out * L.k;
   if (L.ups_cfg >= 0 && h->ups_frames && Lin % 4 == 0 && Lout == Lin * L.s) {
@@ -1123,10 +1184,13 @@ int run_ups(hfg_handle* h, Launcher& ln, const Layer& L, const float* x, int64_t
       q.m_tiles = L.m_tiles_f;
       q.n_tiles = n_tiles;
       q.batch = (int)B;
+      q.amax_in = ain;
+      q.amax_out = aout;
+      q.ew = L.ew;
       q.dbg = h->dbg_flags;
       const char* name = nullptr;
       ln.begin(flop, bytes);
-      hipError_t e = hfg::launch_ups_bf16x3(cfg, h->np, q, ln.stream, &name);
+      hipError_t e = hfg::launch_ups_bf16x3(cfg, h->fmt, h->np, q, ln.stream, &name);
       ln.end(name);
       if (e != hipSuccess)
         return fail(HFG_EIO, "launch %s: %s", L.mod.c_str(), hipGetErrorString(e));
@@ -1156,9 +1220,12 @@ int run_ups(hfg_handle* h, Launcher& ln, const Layer& L, const float* x, int64_t
   p.act_out = 0;
   p.ups_s = L.s;
   p.ups_p = L.p;
-  p.ups_swz = h->ups_swizzle;
+  p.ups_swz = 1;
   p.L_out = (int)Lout;
   p.n_chunks = L.n_chunks;
+  p.amax_in = ain;
+  p.amax_out = aout;
+  p.ew = L.ew;
   p.dbg = h->dbg_flags;
   const int ntile = L.prec == 1 ? hfg::kBf16x3Tiles[L.tile].NTILE() : kTiles[L.tile].NTILE();
   int n_tiles = (p.N + ntile - 1) / ntile, m_tiles = L.m_tiles;
@@ -1166,8 +1233,8 @@ int run_ups(hfg_handle* h, Launcher& ln, const Layer& L, const float* x, int64_t
   const char* name = nullptr;
   ln.begin(flop, bytes);
   hipError_t e = L.prec == 1
-                     ? hfg::launch_conv_bf16x3(tile, L.KT, true, h->np, p, n_tiles, m_tiles, (int)B,
-                                               ln.stream, &name)
+                     ? hfg::launch_conv_bf16x3(tile, L.KT, true, h->fmt, h->np, p, n_tiles, m_tiles,
+                                               (int)B, ln.stream, &name)
                      : hfg::launch_conv((TileId)L.tile, L.KT, true, p, n_tiles, L.m_tiles, (int)B,
                                         ln.stream, &name);
   ln.end(name);
@@ -1177,7 +1244,7 @@ int run_ups(hfg_handle* h, Launcher& ln, const Layer& L, const float* x, int64_t
 
 // A thin stage's whole MRF (or ResBlock only_j alone) in one mrf_thin launch.
 int run_thin(hfg_handle* h, Launcher& ln, const Stage& st, const float* X, int64_t B, int64_t Lt,
-             float* out, const int32_t* lens, int only_j) {
+             float* out, const int32_t* lens, int only_j, uint32_t* aout) {
   const hfg_config& c = h->cfg;
   const int C = st.C;
   hfg::ThinParams p{};
@@ -1202,6 +1269,7 @@ int run_thin(hfg_handle* h, Launcher& ln, const Stage& st, const float* X, int64
     const int q = e - cv_base;
     p.kt[q] = L.k;
     p.dil[q] = L.dil;
+    p.ew[q] = L.ew;
     p.w_off[q] = (int)st.thin_w_off[e];
     flop += 2.0 * C * C * L.k * (double)Lt * B;
     wbytes += 4.0 * C * C * L.k;
@@ -1212,6 +1280,7 @@ int run_thin(hfg_handle* h, Launcher& ln, const Stage& st, const float* X, int64
   p.W = (st.thin_mfma ? hfg::thin_mfma_window(C) : hfg::thin_window(C)) - 2 * halo;
   p.y = out;
   p.div = (float)p.n_res;
+  p.amax_out = aout;
   if (st.thin_mfma) {
     const int base = st.thin_m_conv[cv_base];
     p.wm = reinterpret_cast<const __bf16*>(h->packed_dev + st.thin_m_off) + base / 2;
@@ -1222,39 +1291,41 @@ int run_thin(hfg_handle* h, Launcher& ln, const Stage& st, const float* X, int64
   const double bytes = 8.0 * B * Lt * C + wbytes;  // x once, y once, weights once
   const char* name = nullptr;
   ln.begin(flop, bytes);
-  hipError_t e = st.thin_mfma ? hfg::launch_mrf_thin_mfma(C, h->np, p, (int)B, ln.stream, &name)
+  hipError_t e = st.thin_mfma ? hfg::launch_mrf_thin_mfma(C, h->fmt, h->np, p, (int)B, ln.stream, &name)
                                : hfg::launch_mrf_thin(C, p, (int)B, ln.stream, &name);
   ln.end(name);
   if (e != hipSuccess) return fail(HFG_EIO, "launch mrf_thin (C=%d): %s", C, hipGetErrorString(e));
   return HFG_OK;
 }
 
-// MRF of stage st (models/hifigan.py:116-131) on X [B][C][L]: out = mean_j ResBlock_j(X)
-// (ResBlock.forward :72-86), or out = ResBlock_only_j(X) alone when only_j >= 0.  R and Tb
-// are B*C*L-float scratch buffers of the layer-per-launch ResBlocks; out must not alias X.
 // ResBlock j of stage st (ResBlock.forward, models/hifigan.py:72-86) on X, its result
 // combined into out by the MRF epilogue mode (bit0 add, bit1 divide by n_res); idx = index
 // of its first dilation in st.conv1 / st.conv2.  R, Tb: scratch of the layer-per-launch path.
+// f16x3: ax = scale slot of X; aout = slot of out (committed by the write that completes it)
 int run_one_rb(hfg_handle* h, Launcher& ln, const Stage& st, int j, int idx, const float* X,
                int64_t B, int64_t L, float* R, float* Tb, float* out, int mode,
-               const int32_t* lens) {
+               const int32_t* lens, const uint32_t* ax, uint32_t* aout) {
   const hfg_config& c = h->cfg;
   if (st.rbs[j].fused)
-    return run_resblock(h, ln, st.rbs[j], X, B, L, out, mode, (float)c.n_res, lens, Tb);
+    return run_resblock(h, ln, st.rbs[j], X, B, L, out, mode, (float)c.n_res, lens, Tb, aout);
   int rc;
+  const uint32_t* asrc = ax;
   for (int m = 0; m < c.n_dil[j]; ++m, ++idx) {
     const float* src = (m == 0) ? X : R;
     const Layer& L1 = h->layers[st.conv1[idx]];
     const Layer& L2 = h->layers[st.conv2[idx]];
     // xt = lrelu(conv1(lrelu(x)))
-    rc = run_conv(h, ln, L1, src, B, L, Tb, true, true, nullptr, nullptr, 0, 1.f, lens);
+    uint32_t* at = ln.take();
+    rc = run_conv(h, ln, L1, src, B, L, Tb, true, true, nullptr, nullptr, 0, 1.f, lens, asrc, at);
     if (rc) return rc;
     if (m < c.n_dil[j] - 1) {
       // x = x + conv2(xt)
-      rc = run_conv(h, ln, L2, Tb, B, L, R, false, false, src, nullptr, 0, 1.f, lens);
+      uint32_t* ar = ln.take();
+      rc = run_conv(h, ln, L2, Tb, B, L, R, false, false, src, nullptr, 0, 1.f, lens, at, ar);
+      asrc = ar;
     } else {
       rc = run_conv(h, ln, L2, Tb, B, L, nullptr, false, false, src, out, mode, (float)c.n_res,
-                    lens);
+                    lens, at, aout);
     }
     if (rc) return rc;
   }
@@ -1289,11 +1360,12 @@ int rb_streams(hfg_handle* h, int part) {
 // With conc set, the ResBlocks run concurrently (ResBlock j > 0 on aux stream j-1 of this
 // batch part), each into its own output, and one combine launch forms the mean in the
 // sequential schedule's order — bitwise the same result, for grids that leave CUs idle.
+// ax: f16x3 scale slot of X; aout: slot of out (the MRF mean, or ResBlock only_j's output)
 int run_mrf(hfg_handle* h, Launcher& ln, const Stage& st, const float* X, int64_t B, int64_t L,
             float* R, float* Tb, float* out, const int32_t* lens, int only_j,
-            const RbConc* conc = nullptr) {
+            const uint32_t* ax, uint32_t* aout, const RbConc* conc = nullptr) {
   const hfg_config& c = h->cfg;
-  if (st.thin) return run_thin(h, ln, st, X, B, L, out, lens, only_j);
+  if (st.thin) return run_thin(h, ln, st, X, B, L, out, lens, only_j, aout);
   int rc;
   if (conc && only_j < 0 && c.n_res > 1) {
     if ((rc = rb_streams(h, ln.part))) return rc;
@@ -1303,8 +1375,10 @@ int run_mrf(hfg_handle* h, Launcher& ln, const Stage& st, const float* X, int64_
     if (e != hipSuccess) return hip_fail(e, "ResBlock fork");
     int idx = 0;
     for (int j = 0; j < c.n_res; ++j) {
-      Launcher lj{h, j == 0 ? ln.stream : h->rb_aux[ln.part][j - 1], ln.part, ln.seq, c.n_res};
-      rc = run_one_rb(h, lj, st, j, idx, X, B, L, conc->R[j], conc->Tb[j], conc->O[j], 0, lens);
+      Launcher lj{h, j == 0 ? ln.stream : h->rb_aux[ln.part][j - 1], ln.part, ln.seq, c.n_res,
+                  ln.sl};
+      rc = run_one_rb(h, lj, st, j, idx, X, B, L, conc->R[j], conc->Tb[j], conc->O[j], 0, lens,
+                      ax, nullptr);
       if (rc) return rc;
       ln.seq = lj.seq;
       idx += c.n_dil[j];
@@ -1322,6 +1396,7 @@ int run_mrf(hfg_handle* h, Launcher& ln, const Stage& st, const float* X, int64_
     a.len = lens;
     a.y = out;
     a.div = (float)c.n_res;
+    a.amax_out = aout;
     ln.begin(0.0, 4.0 * B * L * st.C * (c.n_res + 1));
     e = hfg::launch_mrf_combine(a, (int)B, ln.stream);
     ln.end("mrf_combine");
@@ -1335,7 +1410,9 @@ int run_mrf(hfg_handle* h, Launcher& ln, const Stage& st, const float* X, int64_
       continue;
     }
     const int mode = only_j >= 0 ? 0 : ((j > 0 ? 1 : 0) | (j == c.n_res - 1 ? 2 : 0));
-    rc = run_one_rb(h, ln, st, j, idx, X, B, L, R, Tb, out, mode, lens);
+    // the write that completes out: the last ResBlock's (the divide), or only_j's
+    rc = run_one_rb(h, ln, st, j, idx, X, B, L, R, Tb, out, mode, lens, ax,
+                    (only_j >= 0 || (mode & 2)) ? aout : nullptr);
     if (rc) return rc;
     idx += c.n_dil[j];
   }
@@ -1381,9 +1458,21 @@ int forward_impl(hfg_handle* h, const float* mel, int64_t B, int64_t T, const hf
   float* R = buf[1];    // running ResBlock state (also conv_pre output)
   float* Tb = buf[2];   // conv1 output
   float* MRF = buf[3];  // MRF accumulator
+  Slots sl;
   Launcher ln{h, stream, part};
+  ln.sl = &sl;
   const hfg_config& c = h->cfg;
   int rc;
+  if (h->fmt == hfg::kFmtF16) {
+    // after the activation buffers and the length table (ws_part_bytes)
+    sl.base = reinterpret_cast<uint32_t*>(static_cast<char*>(ws) +
+                                          (size_t)nb * sh.buf_elems * sizeof(float) +
+                                          lens_table_bytes(h, B));
+    sl.n = n_slots(h);
+    sl.B = B;
+    hipError_t e = hipMemsetAsync(sl.base, 0, slots_bytes(h, B), stream);
+    if (e != hipSuccess) return hip_fail(e, "hipMemsetAsync(scale slots)");
+  }
   // ragged batch: per-stage valid lengths, computed on the device from lengths[B]
   const int32_t* lt = nullptr;  // lt + s*B = lengths after s upsample stages
   if (user_lens) {
@@ -1407,9 +1496,17 @@ int forward_impl(hfg_handle* h, const float* mel, int64_t B, int64_t T, const hf
                                   hipMemcpyDeviceToDevice, stream);
     return e == hipSuccess ? HFG_OK : hip_fail(e, "hipMemcpyAsync(tap)");
   };
+  // f16x3: the mel's per-item max |value| (no kernel produced it)
+  uint32_t* a_mel = ln.take();
+  if (a_mel) {
+    hipError_t e = hfg::launch_absmax(mel, (int64_t)c.n_mels * T, btc ? 1 : T, btc ? c.n_mels : 1,
+                                      c.n_mels, (int)T, lens_at(0), (int)B, a_mel, stream);
+    if (e != hipSuccess) return fail(HFG_EIO, "launch absmax: %s", hipGetErrorString(e));
+  }
   // conv_pre  (models/hifigan.py:238)
+  uint32_t* a_cur = ln.take();
   rc = run_conv(h, ln, h->layers[h->conv_pre], mel, B, T, R, false, false, nullptr, nullptr, 0,
-                1.f, lens_at(0), btc);
+                1.f, lens_at(0), a_mel, a_cur, btc);
   if (rc) return rc;
   if ((rc = tap(0, R, B * c.c0 * T))) return rc;
   const float* cur = R;
@@ -1417,16 +1514,20 @@ int forward_impl(hfg_handle* h, const float* mel, int64_t B, int64_t T, const hf
     const Stage& st = h->stages[i];
     const int64_t Lin = sh.L[i], L = sh.L[i + 1];
     // lrelu -> ups[i]  (models/hifigan.py:244-245)
-    rc = run_ups(h, ln, h->layers[st.conv_ups], cur, B, Lin, L, X, lens_at(i), lens_at(i + 1));
+    uint32_t* a_x = ln.take();
+    rc = run_ups(h, ln, h->layers[st.conv_ups], cur, B, Lin, L, X, lens_at(i), lens_at(i + 1),
+                 a_cur, a_x);
     if (rc) return rc;
     if ((rc = tap(1 + 2 * i, X, B * st.C * L))) return rc;
     // MRF (models/hifigan.py:116-131) of ResBlocks (:72-86)
-    rc = run_mrf(h, ln, st, X, B, L, R, Tb, MRF, lens_at(i + 1), -1,
+    a_cur = ln.take();
+    rc = run_mrf(h, ln, st, X, B, L, R, Tb, MRF, lens_at(i + 1), -1, a_x, a_cur,
                  nb > 4 && stage_conc(h, st, B, L) ? &conc : nullptr);
     if (rc) return rc;
     if ((rc = tap(2 + 2 * i, MRF, B * st.C * L))) return rc;
     cur = MRF;
   }
+  if (sl.overflow) return fail(HFG_EIO, "internal: f16x3 scale slots exhausted");
   // lrelu -> conv_post -> tanh  (models/hifigan.py:254-256)
   {
     const Layer& Lp = h->layers[h->conv_post];
@@ -1435,7 +1536,7 @@ int forward_impl(hfg_handle* h, const float* mel, int64_t B, int64_t T, const hf
     ln.begin(2.0 * Lp.C_in * 7 * (double)L * B, 4.0 * B * L * (Lp.C_in + 1));
     hipError_t e = hfg::launch_conv_post(cur, (int64_t)Lp.C_in * L, Lp.C_in, (int)L,
                                          h->packed_dev + Lp.w_off, h->packed_dev + Lp.b_off, wav,
-                                         lens_at(c.n_up), (int)B, stream, &name, h->post4);
+                                         lens_at(c.n_up), (int)B, stream, &name);
     ln.end(name);
     if (e != hipSuccess) return fail(HFG_EIO, "launch conv_post: %s", hipGetErrorString(e));
   }
@@ -1496,37 +1597,21 @@ int create_impl(const hfg_config* cfg, bool mrf_only, int device, hfg_handle** o
   h->cfg = *cfg;
   h->mrf_only = mrf_only;
   h->device = device;
+#if HFG_ABLATE
   if (const char* dbg = getenv("HFG_DEBUG_FLAGS")) h->dbg_flags = atoi(dbg);
-  if (const char* bt = getenv("HFG_BF16X3_BIGTILE")) {
-    const int v = atoi(bt);
-    if (v == 0 || v == 3) h->big_tile = v;
-  }
+#endif
+  // schedule choices the parity suites compare (each bitwise invisible, or for the fused
+  // ResBlocks a different rounding order): FUSED_RB, RB_SPLIT, SMALL_TILE, RB_CONC, UPS_FRAMES,
+  // SPLIT
   if (const char* fe = getenv("HFG_FUSED_RB")) h->use_fused_rb = atoi(fe) != 0;
-  if (const char* te = getenv("HFG_THIN")) h->thin = atoi(te) != 0;
-  if (const char* tm = getenv("HFG_THIN_MFMA")) h->thin_mfma = atoi(tm);
+  if (const char* sp = getenv("HFG_RB_SPLIT")) h->rb_split = atoi(sp) != 0;
   if (const char* st = getenv("HFG_SMALL_TILE")) h->small_tile = atoi(st);
   if (const char* rc = getenv("HFG_RB_CONC")) h->rb_conc = atoi(rc);
-  if (const char* us = getenv("HFG_UPS_SWIZZLE")) h->ups_swizzle = atoi(us);
-  if (const char* us = getenv("HFG_UPS_SMALL_ROWS")) h->ups_small_rows = atoi(us);
-  if (const char* uf = getenv("HFG_UPS_FRAMES")) h->ups_frames = atoi(uf);
-  if (const char* pq = getenv("HFG_POST4")) h->post4 = atoi(pq) != 0;
-  if (const char* el = getenv("HFG_EPI_LDS")) h->epi_lds = atoi(el);
-  if (const char* ar = getenv("HFG_AREG")) h->areg = atoi(ar) != 0;
+  if (const char* uf = getenv("HFG_UPS_FRAMES")) h->ups_frames = atoi(uf) == 2 ? 2 : 1;
   if (const char* se = getenv("HFG_SPLIT")) h->split = atoi(se);
-  if (const char* sm = getenv("HFG_SPLIT_MIN")) h->split_min_frames = atoll(sm);
-  if (const char* rn = getenv("HFG_RB64_NARROW")) h->rb64_narrow = atoi(rn) != 0;
-  if (const char* sp = getenv("HFG_RB_SPLIT")) h->rb_split = atoi(sp) != 0;
-  if (const char* sm = getenv("HFG_RB_SPLIT_MIN")) h->rb_split_min = atof(sm);
-  if (const char* we = getenv("HFG_RB_WN32")) {
-    const int v = atoi(we);
-    if (v == 4 || v == 8) h->rb_waves_n32 = v;
-  }
-  if (cfg->dtype == HFG_DTYPE_BF16W) {
-    // bf16-valued weights: their lo plane is zero, the kernels skip lo(w) * hi(x) (NP 2
-    // instances exist for the default tiles and the whole-ResBlock / thin kernels)
-    h->np = 2;
-    if (h->big_tile != 3) h->big_tile = 3;
-  }
+  h->fmt = split_fmt(cfg->dtype);
+  // bf16-valued weights: their lo plane is zero, the kernels skip lo(w) * hi(x)
+  if (cfg->dtype == HFG_DTYPE_BF16W) h->np = 2;
   rc = build_layers(h);
   if (rc) {
     delete h;
@@ -1780,7 +1865,7 @@ int mrf_check(hfg_handle* h, const float* x, int64_t B, int64_t L, float* y, voi
 }
 size_t mrf_ws_bytes(const hfg_handle* h, int64_t B, int64_t L) {
   const size_t one = ((sizeof(float) * (size_t)B * h->stages[0].C * (size_t)L) + 255) & ~(size_t)255;
-  return 2 * one;
+  return 2 * one + slots_bytes(h, B);
 }
 int mrf_run(hfg_handle* h, int only_j, const float* x, int64_t B, int64_t L, float* y, void* ws,
             size_t ws_bytes, void* stream) {
@@ -1792,10 +1877,29 @@ int mrf_run(hfg_handle* h, int only_j, const float* x, int64_t B, int64_t L, flo
   if (!g.ok) return fail(HFG_ENODEV, "hipSetDevice(%d) failed", h->device);
   if (h->dirty && (rc = do_commit(h))) return rc;
   ++h->fwd_count;
+  const size_t one = (mrf_ws_bytes(h, B, L) - slots_bytes(h, B)) / 2;
   float* R = static_cast<float*>(ws);
-  float* Tb = R + mrf_ws_bytes(h, B, L) / 2 / sizeof(float);
-  Launcher ln{h, reinterpret_cast<hipStream_t>(stream), 0};
-  return run_mrf(h, ln, h->stages[0], x, B, L, R, Tb, y, nullptr, only_j);
+  float* Tb = R + one / sizeof(float);
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  Slots sl;
+  Launcher ln{h, st, 0};
+  ln.sl = &sl;
+  uint32_t* ax = nullptr;
+  if (h->fmt == hfg::kFmtF16) {
+    // the caller's x: its per-item max |value| by an absmax pass
+    sl.base = reinterpret_cast<uint32_t*>(static_cast<char*>(ws) + 2 * one);
+    sl.n = n_slots(h);
+    sl.B = B;
+    hipError_t e = hipMemsetAsync(sl.base, 0, slots_bytes(h, B), st);
+    if (e != hipSuccess) return hip_fail(e, "hipMemsetAsync(scale slots)");
+    ax = ln.take();
+    e = hfg::launch_absmax(x, (int64_t)h->stages[0].C * L, L, 1, h->stages[0].C, (int)L, nullptr,
+                           (int)B, ax, st);
+    if (e != hipSuccess) return fail(HFG_EIO, "launch absmax: %s", hipGetErrorString(e));
+  }
+  rc = run_mrf(h, ln, h->stages[0], x, B, L, R, Tb, y, nullptr, only_j, ax, nullptr);
+  if (rc == HFG_OK && sl.overflow) return fail(HFG_EIO, "internal: f16x3 scale slots exhausted");
+  return rc;
 }
 }  // namespace
 
@@ -1952,6 +2056,9 @@ int hfg_debug_packed_layer(hfg_handle* h, const char* mod, float* out, size_t ca
       info[9] = L.kind == L_POST ? 0
                 : L.prec == 1    ? hfg::kBf16x3Tiles[L.tile].MT()
                                  : kTiles[L.tile].MT();
+      // the exponents are set by the commit (0 while weights are missing)
+      if (h->dirty && h->fmt == hfg::kFmtF16) (void)do_commit(h);
+      info[10] = L.ew;
     }
     if (!out) return HFG_OK;
     if (h->dirty) {

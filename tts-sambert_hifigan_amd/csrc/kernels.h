@@ -17,6 +17,15 @@ std::mutex& setup_mutex();
 
 constexpr float kLReluSlope = 0.1f;  // F.leaky_relu(x, 0.1), models/hifigan.py:81,83,244,254
 
+// split formats of the split-precision kernels (bf16x3_common.h): bf16 halves (bf16x3) or
+// power-of-two-scaled f16 halves (f16x3; scale exponents clamped to +-kX3ExpMax)
+constexpr int kFmtBf16 = 0;
+constexpr int kFmtF16 = 1;
+constexpr int kX3ExpMax = 60;
+// words per (producer launch, batch item) scale slot: waves fold their max into one of them
+// (spread to avoid same-address atomic serialisation); consumers take the max of all
+constexpr int kAmaxSpread = 64;
+
 // One implicit-GEMM convolution launch:
 //   out[b][m][n] = bias[m] + sum_{ci, j} Wt[m][ci][j] * act_in(x[b][ci][n + off + j*dil])
 // with x zero outside [0, L_in).  Regular Conv1d: m = output channel.
@@ -47,10 +56,22 @@ struct ConvParams {
   int n_chunks;      // ceil(C_in / CK)
   int n_base;        // first GEMM column of this launch (bf16x3 kernel; 0 elsewhere)
   int epi_lds;       // bf16x3 layer kernel: LDS-staged float4 epilogue (epilogue.h)
-  int dbg;           // ablation flags (HFG_DEBUG_FLAGS; 0 in production; wrong results when
-                     // set), bf16x3 kernel: bit0 skip input restaging after the first
-                     // chunk, bit2 no per-chunk barrier, bit3 no epilogue
+  // f16x3 scaling (bf16x3_common.h): amax_in[b] = max |x| of item b (producer slot, null:
+  // unscaled input), ew = the weights' packing exponent; amax_out[b] <- max |stored y|
+  // (null: not committed)
+  const uint32_t* amax_in;
+  uint32_t* amax_out;
+  int ew;
+  int dbg;           // ablation flags (HFG_DEBUG_FLAGS, builds with -DHFG_ABLATE=1 only; wrong
+                     // results when set), bf16x3 kernel: bit0 skip input restaging after the
+                     // first chunk, bit2 no per-chunk barrier, bit3 no epilogue
 };
+
+// kernel ablation switches (timing experiments) exist only in -DHFG_ABLATE=1 builds
+#ifndef HFG_ABLATE
+#define HFG_ABLATE 0
+#endif
+constexpr bool kAblate = HFG_ABLATE != 0;
 
 // Tile configurations of conv1d_mfma_f32 (fp32 MFMA 32x32x2).
 //   MT = 32*WM*WAVES_M rows, NTILE = 32*WN*WAVES_N columns,
@@ -108,7 +129,8 @@ struct Bf16x3Cfg {
   constexpr int threads() const { return 64 * WAVES_M * WAVES_N; }
 };
 constexpr int kBf16x3Tiles_n = 6;
-// 0: 128x256, 2x4 waves of 64x64, 4 taps/chunk, 3-deep weight ring (1 block/CU)
+// 0: (removed in round 4: 128x256, 2x4 waves of 64x64, 3-deep weight ring, 1 block/CU —
+//    slower than tile 3 / 5; the slot keeps the other tiles' indices)
 // 1: 64x256, 1x4 waves of 64x64, 2 taps/chunk (2 blocks/CU)
 // 2: 32x256, 1x4 waves of 32x64, 4 taps/chunk (2 blocks/CU)
 // 3: 128x256, 2x2 waves of 64x128, 2 taps/chunk (2 blocks/CU: one block's epilogue
@@ -141,16 +163,15 @@ constexpr int bf16x3_areg_rows(int kt, const Bf16x3Cfg& t) {
   const int nt = t.threads();
   return (2 * xw_max + nt - 1) / nt * nt / 2;
 }
-inline int bf16x3_tile_for_rows(int M, int big_tile = 0) {
-  return M >= 128 ? big_tile : (M >= 64 ? 1 : (M >= 32 ? 2 : -1));
-}
+inline int bf16x3_tile_for_rows(int M) { return M >= 128 ? 3 : (M >= 64 ? 1 : (M >= 32 ? 2 : -1)); }
 size_t bf16x3_lds_bytes(int tile, int kt, int dil);
 // the bf16x3 layer kernel handles kt taps at dilation dil (else the fp32 kernel runs)
 inline bool bf16x3_supported(int kt, int dil) {
   return dil >= 1 && dil <= kMaxDil && kt >= 1 && kt <= 16 && (kt - 1) * dil <= kBf16x3MaxHalo;
 }
 // np: MFMA products per multiply-add, 3 (bf16x3) or 2 (bf16-valued weights, tiles 1-4)
-hipError_t launch_conv_bf16x3(int tile, int kt, bool ups, int np, const ConvParams& p,
+// fmt: kFmtBf16 (bf16x3) or kFmtF16 (f16x3), bf16x3_common.h
+hipError_t launch_conv_bf16x3(int tile, int kt, bool ups, int fmt, int np, const ConvParams& p,
                               int n_tiles, int m_tiles, int batch, hipStream_t stream,
                               const char** name);
 
@@ -185,11 +206,14 @@ struct UpsParams {
   int64_t y_bs;
   int C_out, L_out, u;
   int m_tiles, n_tiles, batch;
+  const uint32_t* amax_in;  // f16x3: per-item max |x| (producer slot) or null
+  uint32_t* amax_out;       // f16x3: per-item max |y| slot or null
+  int ew;                   // weight packing exponent (f16x3)
   int dbg;               // ablations (HFG_DEBUG_FLAGS, timing only, wrong results): bit9 no
                          // input conversion after group 0, bit10 no input loads after group 0
 };
 size_t ups_lds_bytes(int cfg);
-hipError_t launch_ups_bf16x3(int cfg, int np, const UpsParams& p, hipStream_t stream,
+hipError_t launch_ups_bf16x3(int cfg, int fmt, int np, const UpsParams& p, hipStream_t stream,
                              const char** name);
 
 // ---- whole ResBlock per launch (resblock_bf16x3.hip) ----
@@ -220,6 +244,8 @@ struct RbParams {
   int mrf_mode;          // bit0: add the existing value, bit1: divide by mrf_div
   float mrf_div;
   float mrf_rcp;         // fp32(1 / mrf_div) when fast_div_ok(mrf_div) (exact fma quotient), else 0
+  int ew[kRbMaxConv];    // f16x3: packing exponent of each conv's weights (stream order)
+  uint32_t* amax_out;    // f16x3: per-item max |stored mrf| slot (final MRF write) or null
   int dbg;               // ablations (HFG_DEBUG_FLAGS, wrong results when set): bit4 no MRF
                          // epilogue, bit5 no x loads, bit6 no operand writes
 };
@@ -230,7 +256,7 @@ inline bool fast_div_ok(float d) {
 }
 bool rb_supported(int C, int kt, int waves_n);
 size_t rb_lds_bytes(int C, int waves_n, int n_conv);
-hipError_t launch_resblock_bf16x3(int C, int waves_n, int kt, int np, const RbParams& p,
+hipError_t launch_resblock_bf16x3(int C, int waves_n, int kt, int fmt, int np, const RbParams& p,
                                   int batch, hipStream_t stream, const char** name);
 
 // ---- whole MRF per launch for thin stages, C <= 16 (mrf_thin.hip) ----
@@ -256,13 +282,15 @@ struct ThinParams {
   const __bf16* wm;          // this launch's stream
   int wm_bytes;              // its size (buffer descriptor range)
   int wm_off[kThinMaxConv];  // byte offset of each conv's first k-step
+  int ew[kThinMaxConv];      // f16x3: packing exponent of each conv's weights
+  uint32_t* amax_out;        // per-item max |y| slot (f16x3 consumers) or null
 };
 int thin_window(int C);      // window columns of the C-channel instance (0: unsupported C)
 size_t thin_lds_bytes(int C);
 hipError_t launch_mrf_thin(int C, const ThinParams& p, int batch, hipStream_t stream,
                            const char** name);
-// the same MRF on the bf16 matrix cores in split precision (v_mfma_f32_16x16x32_bf16):
-// 4 waves x kThinMfmaTiles 16-column tiles (a 512-column window), C in {8, 16}
+// the same MRF on the 16x16x32 matrix cores in split precision (bf16x3 / f16x3 products):
+// 4 waves x kThinMfmaTiles 16-column tiles (a 512-column window), C = 16
 constexpr int kThinMfmaTiles = 8;
 // operand buffers of mrf_thin_mfma: 2 = one barrier per conv (conv1 / conv2 alternate),
 // 1 = rewritten in place (two barriers per conv; round 2)
@@ -270,14 +298,10 @@ constexpr int kThinMfmaTiles = 8;
 #define HFG_THIN_BUFS 2
 #endif
 constexpr int kThinMfmaBufs = HFG_THIN_BUFS;
-// C = 8 row-half sum: v_permlane32_swap (1) or a ds_bpermute shuffle (0)
-#ifndef HFG_THIN_SWAP
-#define HFG_THIN_SWAP 1
-#endif
-constexpr int kThinMfmaMaxSteps = 4;  // k-steps per conv (k <= 7 for C = 16, <= 15 for C = 8)
+constexpr int kThinMfmaMaxSteps = 4;  // k-steps per conv (k <= 7 at C = 16)
 int thin_mfma_window(int C);  // 0: unsupported C
 size_t thin_mfma_lds_bytes(int C);
-hipError_t launch_mrf_thin_mfma(int C, int np, const ThinParams& p, int batch,
+hipError_t launch_mrf_thin_mfma(int C, int fmt, int np, const ThinParams& p, int batch,
                                 hipStream_t stream, const char** name);
 
 // Launch the conv kernel for (tile, taps, ups).  Returns a hipError_t and,
@@ -316,6 +340,7 @@ struct MrfCombineArgs {
   const int32_t* len;
   float* y;
   float div;
+  uint32_t* amax_out;  // per-item max |y| slot (f16x3 consumers) or null
 };
 hipError_t launch_mrf_combine(const MrfCombineArgs& a, int batch, hipStream_t stream);
 
@@ -325,6 +350,11 @@ struct StageLenParams {
   int n_up, T;
   int up_rates[8], up_kernels[8];
 };
+// out[b] <- max(out[b], max |x[b][c][t]|) over c < C, t < len[b] (len null = L): the f16x3
+// scale slot of a tensor no producing kernel reported (the mel, a caller's MRF input)
+hipError_t launch_absmax(const float* x, int64_t x_bs, int64_t x_cs, int64_t x_ts, int C, int L,
+                         const int32_t* len, int batch, uint32_t* out, hipStream_t stream);
+
 hipError_t launch_stage_lengths(const int32_t* lens, int B, const StageLenParams& sp,
                                 int32_t* out, hipStream_t stream);
 

@@ -181,6 +181,7 @@ mrf_thin(const ThinParams p) {             // lgkmcnt(0) waits on the scalar wei
 
   // y = mrf / n_res on the window centre
   float* __restrict__ yb = p.y + (int64_t)b * p.bs;
+  float vmax = 0.f;  // max |stored value| (f16x3 consumers: p.amax_out)
 #pragma unroll
   for (int q = 0; q < NP; ++q)
 #pragma unroll
@@ -189,8 +190,13 @@ mrf_thin(const ThinParams p) {             // lgkmcnt(0) waits on the scalar wei
       const int c = cbase + 64 * i;
       if (!(vk[i] && c >= p.halo && c < p.halo + p.W)) continue;
 #pragma unroll
-      for (int ch = 0; ch < C; ++ch) yb[(unsigned)(ch * p.L + ws + c)] = mrf[ch][q][e] / p.div;
+      for (int ch = 0; ch < C; ++ch) {
+        const float v = mrf[ch][q][e] / p.div;
+        yb[(unsigned)(ch * p.L + ws + c)] = v;
+        vmax = fmaxf(vmax, fabsf(v));
+      }
     }
+  if (p.amax_out) amax_commit(vmax, p.amax_out, b);
 }
 
 namespace {

@@ -21,10 +21,13 @@ namespace {
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 typedef float floatx2 __attribute__((ext_vector_type(2)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 halfx8 __attribute__((ext_vector_type(8)));
 
 constexpr int kOps = 8;  // distinct operand registers cycled through
 
-// kind 0: v_mfma_f32_32x32x16_bf16 (32768 flop); kind 1: v_mfma_f32_32x32x2_f32 (4096 flop).
+// kind 0: v_mfma_f32_32x32x16_bf16 (32768 flop); kind 1: v_mfma_f32_32x32x2_f32 (4096 flop);
+// kind 2 (KIND 2 here): v_mfma_f32_32x32x16_f16 on operands with random 10-bit mantissas (the
+// f16x3 kernels' instruction: its multiplier switches more bits per product than bf16's).
 // CHAINS independent accumulators per wave (1: every MFMA accumulates onto the previous
 // one's result, the order of the split-product triples in the conv kernels)
 template <int KIND, int CHAINS>
@@ -44,7 +47,7 @@ __global__ void __launch_bounds__(256, 2) mfma_stream(const uint32_t* __restrict
   for (int c = 0; c < CHAINS; ++c)
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[c][r] = 0.f;
-  if constexpr (KIND == 0) {
+  if constexpr (KIND == 0 || KIND == 2) {
     bf16x8 a[kOps], b[kOps];
 #pragma unroll
     for (int i = 0; i < kOps; ++i) {
@@ -52,6 +55,7 @@ __global__ void __launch_bounds__(256, 2) mfma_stream(const uint32_t* __restrict
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         // bf16 pairs with exponents kept in [2^-8, 2^8) so the chains never overflow
+        // (f16: the same bits are sign + 10 random mantissa bits, exponent 2^0)
         w[e] = (rnd[(gid * 64 + i * 8 + e) & 0xFFFFF] & 0x83FF83FFu) | 0x3C003C00u;
         v[e] = (rnd[(gid * 64 + i * 8 + 4 + e) & 0xFFFFF] & 0x83FF83FFu) | 0x3C003C00u;
       }
@@ -63,7 +67,12 @@ __global__ void __launch_bounds__(256, 2) mfma_stream(const uint32_t* __restrict
       for (int i = 0; i < kOps; ++i)
 #pragma unroll
         for (int c = 0; c < CHAINS; ++c)
-          acc[c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i], b[(i + c + 1) % kOps], acc[c], 0, 0, 0);
+          if constexpr (KIND == 0)
+            acc[c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i], b[(i + c + 1) % kOps], acc[c], 0, 0, 0);
+          else
+            acc[c] = __builtin_amdgcn_mfma_f32_32x32x16_f16(
+                __builtin_bit_cast(halfx8, a[i]), __builtin_bit_cast(halfx8, b[(i + c + 1) % kOps]),
+                acc[c], 0, 0, 0);
     }
   } else {
     float a[kOps], b[kOps];
@@ -95,7 +104,8 @@ __global__ void __launch_bounds__(256, 2) mfma_stream(const uint32_t* __restrict
 }  // namespace
 
 extern "C" int hfg_probe_mfma_rate(int device, int kind, int iters, double* tflops, double* mhz) {
-  if (kind < 0 || kind > 3 || iters <= 0 || !tflops || !mhz) return HFG_EINVAL;
+  // kind 0 bf16, 1 fp32, 2 bf16 one chain, 3 fp32 one chain, 4 f16, 5 f16 one chain
+  if (kind < 0 || kind > 5 || iters <= 0 || !tflops || !mhz) return HFG_EINVAL;
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n) return HFG_ENODEV;
   int prev = 0;
@@ -140,7 +150,9 @@ extern "C" int hfg_probe_mfma_rate(int device, int kind, int iters, double* tflo
       if (kind == 0) mfma_stream<0, 4><<<blocks, 256, 0, st>>>(rnd, it, sink, clk);
       else if (kind == 1) mfma_stream<1, 4><<<blocks, 256, 0, st>>>(rnd, it, sink, clk);
       else if (kind == 2) mfma_stream<0, 1><<<blocks, 256, 0, st>>>(rnd, it, sink, clk);
-      else mfma_stream<1, 1><<<blocks, 256, 0, st>>>(rnd, it, sink, clk);
+      else if (kind == 3) mfma_stream<1, 1><<<blocks, 256, 0, st>>>(rnd, it, sink, clk);
+      else if (kind == 4) mfma_stream<2, 4><<<blocks, 256, 0, st>>>(rnd, it, sink, clk);
+      else mfma_stream<2, 1><<<blocks, 256, 0, st>>>(rnd, it, sink, clk);
     };
     launch(iters / 4 > 0 ? iters / 4 : 1);  // warm the clocks up
     (void)hipEventRecord(e0, st);
@@ -155,8 +167,10 @@ extern "C" int hfg_probe_mfma_rate(int device, int kind, int iters, double* tflo
       rc = HFG_EIO;
       goto done;
     }
-    const double flop_per = (kind & 1) == 0 ? 32768.0 : 4096.0;
-    const double flop = flop_per * kOps * (kind < 2 ? 4 : 1) * (double)iters * blocks * 4;
+    const bool f32 = kind == 1 || kind == 3;
+    const double flop_per = f32 ? 4096.0 : 32768.0;
+    const int chains = (kind == 0 || kind == 1 || kind == 4) ? 4 : 1;
+    const double flop = flop_per * kOps * chains * (double)iters * blocks * 4;
     *tflops = ms > 0.f ? flop / (ms * 1e-3) / 1e12 : 0.0;
     *mhz = clk_h[1] ? (double)clk_h[0] / ((double)clk_h[1] / 100.0) : 0.0;  // realtime: 100 MHz
   }

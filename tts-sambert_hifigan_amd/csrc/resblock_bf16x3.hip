@@ -44,7 +44,7 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 typedef float floatx2 __attribute__((ext_vector_type(2)));
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 
-template <int KT, int WAVES_M, int WAVES_N, int NP>
+template <int KT, int WAVES_M, int WAVES_N, int NP, int FMT>
 __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N, 2)  // 2 waves/SIMD: <= 256 VGPRs
 resblock_bf16x3(const RbParams p) {
   constexpr int NW = WAVES_M * WAVES_N;
@@ -66,6 +66,8 @@ resblock_bf16x3(const RbParams p) {
 
   extern __shared__ __attribute__((aligned(16))) char lds[];
   float* const bias_s = reinterpret_cast<float*>(lds + NG * GS);
+  // f16x3: per-wave max |next operand| (NW floats after the biases)
+  float* const amax_s = bias_s + p.n_conv * C;
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -136,7 +138,7 @@ resblock_bf16x3(const RbParams p) {
     }
     // ablation bit 5 zeroes x after the loads (a select on a uniform flag inside the load
     // expression made the compiler branch per element)
-    const bool xz = dbg & 32;
+    const bool xz = kAblate && (dbg & 32);
 #pragma unroll
     for (int k = 0; k < WN; ++k)
 #pragma unroll
@@ -154,11 +156,12 @@ resblock_bf16x3(const RbParams p) {
   // B operand of the next conv: lrelu(v), zero outside [0, len), split hi/lo -> LDS.
   // The 8 accumulator rows a lane holds per 16-channel group are exactly the 8 slots
   // (one 16-B row of its half-group) it reads as a B fragment.
-  auto write_operand = [&](const floatx16 (&v)[WN]) {
-    if (dbg & 64) return;
+  // f16x3: the operand is scaled by sc = 2^e (block_exp) inside the same two factors
+  auto write_operand = [&](const floatx16 (&v)[WN], float sc) {
+    if (kAblate && (dbg & 64)) return;
 #pragma unroll
     for (int k = 0; k < WN; ++k) {
-      const floatx2 f1k = vk[k] ? 1.0f : 0.0f, f2k = vk[k] ? kLReluSlope : 0.0f;
+      const floatx2 f1k = vk[k] ? sc : 0.0f, f2k = vk[k] ? kLReluSlope * sc : 0.0f;
 #pragma unroll
       for (int gg = 0; gg < 2; ++gg) {
         bf16x8 h, l;
@@ -170,9 +173,8 @@ resblock_bf16x3(const RbParams p) {
           const floatx2 p1 = vv * f1k, p2 = vv * f2k;  // v_pk_mul_f32
           a[0] = fmaxf(p1[0], p2[0]);
           a[1] = fmaxf(p1[1], p2[1]);
-          const bf16x2 hh = __builtin_convertvector(a, bf16x2);
-          const floatx2 hf = __builtin_convertvector(hh, floatx2);
-          const bf16x2 ll = __builtin_convertvector(a - hf, bf16x2);
+          bf16x2 hh, ll;
+          split2<FMT>(a, hh, ll);
           h[e] = hh[0];
           h[e + 1] = hh[1];
           l[e] = ll[0];
@@ -184,7 +186,40 @@ resblock_bf16x3(const RbParams p) {
       }
     }
   };
-  write_operand(xcur);
+  // f16x3: the block's largest |value| over the window's exact columns sets the power-of-two
+  // scale of each operand it writes (per block: the window of an item, and so the result, is
+  // the same whatever else is in the batch).  Exact = inside [0, len) and at least `radius`
+  // (the receptive-field radius of the convs run so far) from the window edges: the garbage
+  // columns outside read the never-written margin rows (stale LDS), so counting them would
+  // make the scale depend on earlier launches; garbage that overflows f16 stays in garbage
+  // columns.  Each wave posts its max before the barrier that ends every read of the previous
+  // operand, and all read the NW maxima after it.
+  auto wave_amax = [&](const floatx16 (&v)[WN], int radius) {
+    float m = 0.f;
+#pragma unroll
+    for (int k = 0; k < WN; ++k) {
+      const int c = cbase + 32 * k + col;
+      const bool ex_k = vk[k] && c >= radius && c < NWIN - radius;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) m = ex_k ? fmaxf(m, fabsf(v[k][r])) : m;
+    }
+    m = wave_max(m);
+    if (lane == 0) amax_s[wave] = m;
+  };
+  auto block_exp = [&]() {
+    float m = amax_s[0];
+#pragma unroll
+    for (int w = 1; w < NW; ++w) m = fmaxf(m, amax_s[w]);
+    return x3_exp(m);
+  };
+  int ex = 0;
+  int radius = 0;  // f16x3: receptive-field radius of the convs run so far
+  if constexpr (FMT == kFmtF16) {
+    wave_amax(xcur, 0);
+    lds_barrier();
+    ex = block_exp();
+  }
+  write_operand(xcur, exp2i(ex));
   lds_barrier();
 
   // conv cv over the whole window: acc = bias + W_cv * operand (one LDS barrier at the
@@ -195,7 +230,8 @@ resblock_bf16x3(const RbParams p) {
     const int pad = (KT - 1) / 2 * d;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      const float bv = bias_s[cv * C + row0 + rrow(r)];
+      // f16x3: the bias joins after the unscale (finalize)
+      const float bv = FMT == kFmtF16 ? 0.f : bias_s[cv * C + row0 + rrow(r)];
 #pragma unroll
       for (int k = 0; k < WN; ++k) acc[k][r] = bv;
     }
@@ -222,9 +258,9 @@ resblock_bf16x3(const RbParams p) {
 #pragma unroll
       for (int k = 0; k < WN; ++k) {
         if constexpr (NP == 3)  // the weights' lo plane (zero for bf16-valued weights: NP 2)
-          acc[k] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ra_l[cur], bh[cur][k], acc[k], 0, 0, 0);
-        acc[k] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ra_h[cur], bl[cur][k], acc[k], 0, 0, 0);
-        acc[k] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ra_h[cur], bh[cur][k], acc[k], 0, 0, 0);
+          acc[k] = mfma32<FMT>(ra_l[cur], bh[cur][k], acc[k]);
+        acc[k] = mfma32<FMT>(ra_h[cur], bl[cur][k], acc[k]);
+        acc[k] = mfma32<FMT>(ra_h[cur], bh[cur][k], acc[k]);
       }
       load_a(cur, qb + s + 2);
       if (s + 1 < STEPS) {
@@ -239,27 +275,65 @@ resblock_bf16x3(const RbParams p) {
       __builtin_amdgcn_sched_group_barrier(0x008, NP * WN, 0);  // rest of the MFMAs
       __builtin_amdgcn_sched_barrier(0);
     }
-    lds_barrier();
+  };
+  // f16x3: acc = acc * 2^-(e_x + e_w) + bias (exact unscale, one rounding for the bias)
+  auto finalize = [&](int cv) {
+    const float inv = exp2i(-(ex + p.ew[cv]));
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const float bv = bias_s[cv * C + row0 + rrow(r)];
+#pragma unroll
+      for (int k = 0; k < WN; ++k) acc[k][r] = __builtin_fmaf(acc[k][r], inv, bv);
+    }
   };
 
   // dilation pairs: xt = lrelu(conv1(lrelu(x)) + b1); x = x + (conv2(xt) + b2)
-  for (int cv = 0; cv < n_conv; cv += 2) {
-    run_conv(cv);
-    write_operand(acc);
-    lds_barrier();
-    run_conv(cv + 1);
-#pragma unroll
-    for (int k = 0; k < WN; ++k)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) xcur[k][r] = xcur[k][r] + acc[k][r];
-    if (cv + 2 < n_conv) {
-      write_operand(xcur);
+  if constexpr (FMT == kFmtBf16) {
+    for (int cv = 0; cv < n_conv; cv += 2) {
+      run_conv(cv);
       lds_barrier();
+      write_operand(acc, 1.0f);
+      lds_barrier();
+      run_conv(cv + 1);
+      lds_barrier();
+#pragma unroll
+      for (int k = 0; k < WN; ++k)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) xcur[k][r] = xcur[k][r] + acc[k][r];
+      if (cv + 2 < n_conv) {
+        write_operand(xcur, 1.0f);
+        lds_barrier();
+      }
+    }
+  } else {
+    for (int cv = 0; cv < n_conv; cv += 2) {
+      run_conv(cv);
+      finalize(cv);
+      radius += (KT - 1) / 2 * p.dil[cv];
+      wave_amax(acc, radius);
+      lds_barrier();  // every wave is done reading the operand; the maxima are posted
+      ex = block_exp();
+      write_operand(acc, exp2i(ex));
+      lds_barrier();
+      run_conv(cv + 1);
+      finalize(cv + 1);
+      radius += (KT - 1) / 2;  // conv2: dilation 1
+#pragma unroll
+      for (int k = 0; k < WN; ++k)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) xcur[k][r] = xcur[k][r] + acc[k][r];
+      if (cv + 2 < n_conv) {
+        wave_amax(xcur, radius);
+        lds_barrier();
+        ex = block_exp();
+        write_operand(xcur, exp2i(ex));
+        lds_barrier();
+      }
     }
   }
 
   // ---- MRF: (mrf + x) [/ n_res] on the window centre ----
-  if (dbg & 16) {  // ablation: no MRF epilogue
+  if (kAblate && (dbg & 16)) {  // ablation: no MRF epilogue
     if (xcur[0][0] == 1.2345e-30f) p.mrf[0] = xcur[WN - 1][15];
     return;
   }
@@ -318,6 +392,14 @@ resblock_bf16x3(const RbParams p) {
       }
     }
   }
+  if (p.amax_out) {  // f16x3 consumers of the stage output (block-uniform branch)
+    float m = 0.f;
+#pragma unroll
+    for (int k = 0; k < WN; ++k)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) m = ok[k] ? fmaxf(m, fabsf(xcur[k][r])) : m;
+    amax_commit(m, p.amax_out, b);
+  }
 }
 
 namespace {
@@ -325,22 +407,23 @@ namespace {
 typedef void (*RbFn)(const RbParams);
 
 struct EntryRb {
-  int kt, waves_m, waves_n, np;
+  int kt, waves_m, waves_n, np, fmt;
   RbFn fn;
   char name[64];
 };
 
-#define HFGRB_ENTRY(KT, WMS, WNS, NP) \
-  { KT, WMS, WNS, NP, resblock_bf16x3<KT, WMS, WNS, NP>, {0} }
-#define HFGRB_KTS(WMS, WNS, NP)                                                                 \
-  HFGRB_ENTRY(3, WMS, WNS, NP), HFGRB_ENTRY(5, WMS, WNS, NP), HFGRB_ENTRY(7, WMS, WNS, NP), \
-      HFGRB_ENTRY(11, WMS, WNS, NP)
+#define HFGRB_ENTRY(KT, WMS, WNS, NP, FMT) \
+  { KT, WMS, WNS, NP, FMT, resblock_bf16x3<KT, WMS, WNS, NP, FMT>, {0} }
+#define HFGRB_KTS(WMS, WNS, NP, FMT)                                                  \
+  HFGRB_ENTRY(3, WMS, WNS, NP, FMT), HFGRB_ENTRY(5, WMS, WNS, NP, FMT),               \
+      HFGRB_ENTRY(7, WMS, WNS, NP, FMT), HFGRB_ENTRY(11, WMS, WNS, NP, FMT)
+// C = 64 (2 x 4 waves), C = 32 (1 x 4), C = 128 (4 x 2, k = 3), C = 64 narrow (2 x 2, k = 3)
+#define HFGRB_SET(NP, FMT)                                                            \
+  HFGRB_KTS(2, 4, NP, FMT), HFGRB_KTS(1, 4, NP, FMT), HFGRB_ENTRY(3, 4, 2, NP, FMT),   \
+      HFGRB_ENTRY(3, 2, 2, NP, FMT)
 
-// NP 3: bf16x3 products; NP 2: bf16-valued weights (HFG_DTYPE_BF16W)
-EntryRb g_entriesRb[] = {HFGRB_KTS(2, 4, 3), HFGRB_KTS(1, 8, 3), HFGRB_KTS(1, 4, 3),
-                         HFGRB_ENTRY(3, 4, 2, 3), HFGRB_ENTRY(3, 2, 2, 3),
-                         HFGRB_KTS(2, 4, 2), HFGRB_KTS(1, 8, 2), HFGRB_KTS(1, 4, 2),
-                         HFGRB_ENTRY(3, 4, 2, 2), HFGRB_ENTRY(3, 2, 2, 2)};
+// bf16x3 (NP 3, bf16), f16x3 (NP 3, f16), bf16w (NP 2 on the f16 kernels)
+EntryRb g_entriesRb[] = {HFGRB_SET(3, 0), HFGRB_SET(3, 1), HFGRB_SET(2, 1)};
 
 }  // namespace
 
@@ -349,21 +432,24 @@ bool rb_supported(int C, int kt, int waves_n) {
   const int wm = C / 32;
   if (C % 32 != 0) return false;
   for (auto& e : g_entriesRb)
-    if (e.kt == kt && e.waves_m == wm && e.waves_n == waves_n && e.np == 3) return true;
+    if (e.kt == kt && e.waves_m == wm && e.waves_n == waves_n && e.np == 3 && e.fmt == 0) return true;
   return false;
 }
 
 size_t rb_lds_bytes(int C, int waves_n, int n_conv) {
   const size_t rows = (size_t)kRbColsPerWave * waves_n + 2 * rb_marg(C, waves_n);
-  return (size_t)C * rows * 4 + sizeof(float) * (size_t)n_conv * C;
+  // operand planes, biases, the per-wave maxima of f16x3 (<= 16 waves)
+  return (size_t)C * rows * 4 + sizeof(float) * ((size_t)n_conv * C + 16);
 }
 
-hipError_t launch_resblock_bf16x3(int C, int waves_n, int kt, int np, const RbParams& p,
+hipError_t launch_resblock_bf16x3(int C, int waves_n, int kt, int fmt, int np, const RbParams& p,
                                   int batch, hipStream_t stream, const char** name) {
   const int wm = C / 32;
   EntryRb* e = nullptr;
   for (auto& cand : g_entriesRb)
-    if (cand.kt == kt && cand.waves_m == wm && cand.waves_n == waves_n && cand.np == np) e = &cand;
+    if (cand.kt == kt && cand.waves_m == wm && cand.waves_n == waves_n && cand.np == np &&
+        cand.fmt == fmt)
+      e = &cand;
   if (!e || C % 32 != 0) return hipErrorInvalidValue;
   const int nwin = kRbColsPerWave * waves_n;
   if (p.n_conv < 2 || p.n_conv > kRbMaxConv || (p.n_conv & 1)) return hipErrorInvalidValue;
@@ -374,8 +460,8 @@ hipError_t launch_resblock_bf16x3(int C, int waves_n, int kt, int np, const RbPa
   {
     std::lock_guard<std::mutex> lk(setup_mutex());
     if (!e->name[0])
-      snprintf(e->name, sizeof(e->name), "resblock_bf16x3<%d, %d, %d, %d>", e->kt, e->waves_m,
-               e->waves_n, e->np);
+      snprintf(e->name, sizeof(e->name), "resblock_bf16x3<%d, %d, %d, %d, %d>", e->kt, e->waves_m,
+               e->waves_n, e->np, e->fmt);
   }
   const size_t lds = rb_lds_bytes(C, waves_n, p.n_conv);
   if (lds > 160 * 1024) return hipErrorInvalidValue;

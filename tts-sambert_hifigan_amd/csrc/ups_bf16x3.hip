@@ -59,7 +59,7 @@ typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 template <int WAVES_M, int WAVES_N, int WM, int WN>
 constexpr int ups_min_blocks() { return WAVES_M * WM * WN <= 2 ? HFG_UPS_SMALL_OCC : 2; }
 
-template <int WAVES_M, int WAVES_N, int WM, int WN, int NP>
+template <int WAVES_M, int WAVES_N, int WM, int WN, int NP, int FMT>
 __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N, (ups_min_blocks<WAVES_M, WAVES_N, WM, WN>()))
 ups_bf16x3(const UpsParams p) {
   constexpr int NW = WAVES_M * WAVES_N;
@@ -105,6 +105,9 @@ ups_bf16x3(const UpsParams p) {
     b = __builtin_amdgcn_readfirstlane(b);
   }
   const int T_b = p.len_in ? min(p.len_in[b], p.T) : p.T;
+  // f16x3 (bf16x3_common.h): input scale from the producer's per-item max, unscale after
+  const int ex = FMT == kFmtF16 ? x3_exp_slot(p.amax_in, b) : 0;
+  const float sx = FMT == kFmtF16 ? exp2i(ex) : 1.0f;
   const int m0 = tx * NTILE;
   if (m0 >= T_b) return;  // whole tile past this utterance's end (block-uniform)
   const int NG = p.C_in / 16;
@@ -133,15 +136,13 @@ ups_bf16x3(const UpsParams p) {
   const int hf = task / NQ;                  // channel half of the task
   const int xq = task - hf * NQ;             // quad of the task
   const int t0 = m0 - 4 + 4 * xq;            // first frame of the quad
-  // zero padding and leaky_relu as max(v * s1, v * s2): (1, 0.1) inside [0, T_b), (0, 0)
-  // outside (bitwise the polyphase kernel's staging)
-  float s1[4], s2[4];
+  // leaky_relu as max(v * sx, v * 0.1 sx) (f16x3 scale sx; bitwise max(v, 0.1 v) for bf16x3)
+  // and the zero padding as a select: frames in [T_b, L) of a ragged item were never written
+  // (0 * NaN would be NaN), and the polyphase kernel reads no such frame
+  const float sx1 = kLReluSlope * sx;
+  bool okt[4];
 #pragma unroll
-  for (int tt = 0; tt < 4; ++tt) {
-    const bool ok = has_task && (unsigned)(t0 + tt) < (unsigned)T_b;
-    s1[tt] = ok ? 1.0f : 0.0f;
-    s2[tt] = ok ? kLReluSlope : 0.0f;
-  }
+  for (int tt = 0; tt < 4; ++tt) okt[tt] = has_task && (unsigned)(t0 + tt) < (unsigned)T_b;
   // whole quads only (L % 4 == 0, host-checked): a quad is inside the row or wholly outside
   const bool q_in = has_task && t0 >= 0 && t0 < p.L;
   const unsigned xoff_lane = q_in ? (unsigned)(8 * hf * p.L + t0) * 4u : 0u;
@@ -165,14 +166,10 @@ ups_bf16x3(const UpsParams p) {
 #pragma unroll
       for (int e = 0; e < 8; e += 2) {
         floatx2 a;
-        a[0] = fmaxf(xv[e][tt] * s1[tt], xv[e][tt] * s2[tt]);
-        a[1] = fmaxf(xv[e + 1][tt] * s1[tt], xv[e + 1][tt] * s2[tt]);
-        const bf16x2 hh = __builtin_convertvector(a, bf16x2);
-        const floatx2 hfl = __builtin_convertvector(hh, floatx2);
-        floatx2 d;
-        d[0] = a[0] - hfl[0];
-        d[1] = a[1] - hfl[1];
-        const bf16x2 ll = __builtin_convertvector(d, bf16x2);
+        a[0] = okt[tt] ? fmaxf(xv[e][tt] * sx, xv[e][tt] * sx1) : 0.f;
+        a[1] = okt[tt] ? fmaxf(xv[e + 1][tt] * sx, xv[e + 1][tt] * sx1) : 0.f;
+        bf16x2 hh, ll;
+        split2<FMT>(a, hh, ll);
         hv[e] = hh[0];
         hv[e + 1] = hh[1];
         lv[e] = ll[0];
@@ -208,7 +205,7 @@ ups_bf16x3(const UpsParams p) {
     const bool more = g + 1 < NG;  // block-uniform
     if (more) {
       issue_a(g + 1, (g + 1) & 1);
-      if (!(p.dbg & 1024)) load_x(g + 1);
+      if (!(kAblate && (p.dbg & 1024))) load_x(g + 1);
     }
     // A fragments of both classes and taps: [class][tap][plane][wm]
     const char* as = Abuf + (g & 1) * SLAB;
@@ -243,21 +240,33 @@ ups_bf16x3(const UpsParams p) {
           for (int tp = 0; tp < 2; ++tp) {
             const int o = c + tp;  // class L: offsets -1, 0 (o = 0, 1); class R: 0, +1 (1, 2)
             if constexpr (NP == 3)
-              acc[c][i][k] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[c][tp][1][i], bh[o],
-                                                                    acc[c][i][k], 0, 0, 0);
-            acc[c][i][k] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[c][tp][0][i], bl[o],
-                                                                  acc[c][i][k], 0, 0, 0);
-            acc[c][i][k] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[c][tp][0][i], bh[o],
-                                                                  acc[c][i][k], 0, 0, 0);
+              acc[c][i][k] = mfma32<FMT>(a[c][tp][1][i], bh[o],
+                                                                    acc[c][i][k]);
+            acc[c][i][k] = mfma32<FMT>(a[c][tp][0][i], bl[o],
+                                                                  acc[c][i][k]);
+            acc[c][i][k] = mfma32<FMT>(a[c][tp][0][i], bh[o],
+                                                                  acc[c][i][k]);
           }
     }
-    if (more && !(p.dbg & 512)) store_x((g + 1) & 1);
+    if (more && !(kAblate && (p.dbg & 512))) store_x((g + 1) & 1);
     wait_vm<0>();
     lds_barrier();
   }
 
+  if constexpr (FMT == kFmtF16) {
+    const float inv = exp2i(-(ex + p.ew));
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int i = 0; i < WM; ++i)
+#pragma unroll
+        for (int k = 0; k < WN; ++k) acc[c][i][k] = acc[c][i][k] * inv;
+  }
+
   // ---- epilogue: bias, stores of whole sample runs ----
   float* yb = p.y + (int64_t)b * p.y_bs;
+  float vmax = 0.f;  // max |stored value| (f16x3 consumers: p.amax_out)
+  auto t2 = [&](float a, float c) { vmax = fmaxf(vmax, fmaxf(fabsf(a), fabsf(c))); };
   const int h = p.u >> 1;
 #pragma unroll
   for (int i = 0; i < WM; ++i) {
@@ -292,6 +301,8 @@ ups_bf16x3(const UpsParams p) {
             v.z = odd ? l1 : v0;
             v.w = odd ? r1 : v1;
             *reinterpret_cast<float4*>(yb + (int64_t)(odd ? co0 + 1 : co0) * p.L_out + 2 * me) = v;
+            t2(v.x, v.y);
+            t2(v.z, v.w);
           } else {
             // last frame of an odd-length utterance (even lane, its odd partner past T_b):
             // both channels' pairs as 8-B stores
@@ -302,6 +313,8 @@ ups_bf16x3(const UpsParams p) {
             c[1] = r1;
             *reinterpret_cast<floatx2*>(yb + (int64_t)co0 * p.L_out + 2 * m) = a;
             *reinterpret_cast<floatx2*>(yb + (int64_t)(co0 + 1) * p.L_out + 2 * m) = c;
+            t2(l0, r0);
+            t2(l1, r1);
           }
         }
       } else if (h == 1) {
@@ -314,6 +327,7 @@ ups_bf16x3(const UpsParams p) {
           v[0] = acc[0][i][k][r] + bv;
           v[1] = acc[1][i][k][r] + bv;
           *reinterpret_cast<floatx2*>(yb + (int64_t)co * p.L_out + 2 * m) = v;
+          t2(v[0], v[1]);
         }
       } else if (h == 2) {
         // rows (co, 0), (co, 1), (co + 1, 0), (co + 1, 1): samples 4m .. 4m + 3 of co, co + 1
@@ -330,6 +344,8 @@ ups_bf16x3(const UpsParams p) {
             v.z = acc[1][i][k][r0] + bv;
             v.w = acc[1][i][k][r0 + 1] + bv;
             *reinterpret_cast<float4*>(yb + (int64_t)co * p.L_out + 4 * m) = v;
+            t2(v.x, v.y);
+            t2(v.z, v.w);
           }
       } else {
         // h % 4 == 0: 4 consecutive rows = s' .. s' + 3 of one channel, per class
@@ -346,11 +362,14 @@ ups_bf16x3(const UpsParams p) {
             v.z = acc[c][i][k][4 * q + 2] + bv;
             v.w = acc[c][i][k][4 * q + 3] + bv;
             *reinterpret_cast<float4*>(yb + (int64_t)co * p.L_out + m * p.u + c * h + sp) = v;
+            t2(v.x, v.y);
+            t2(v.z, v.w);
           }
         }
       }
     }
   }
+  if (p.amax_out) amax_commit(vmax, p.amax_out, b);
 }
 
 namespace {
@@ -358,23 +377,24 @@ namespace {
 typedef void (*UpsFn)(const UpsParams);
 
 struct EntryUps {
-  int cfg, np;
+  int cfg, np, fmt;
   UpsFn fn;
   char name[64];
 };
 
-#define HFGUPS_ENTRY(CFG, NP)                                                                \
+#define HFGUPS_ENTRY(CFG, NP, FMT)                                                           \
   {                                                                                          \
-    CFG, NP,                                                                                 \
+    CFG, NP, FMT,                                                                            \
         ups_bf16x3<kUpsCfgs[CFG].WAVES_M, kUpsCfgs[CFG].WAVES_N, kUpsCfgs[CFG].WM,          \
-                   kUpsCfgs[CFG].WN, NP>,                                                    \
+                   kUpsCfgs[CFG].WN, NP, FMT>,                                               \
     {                                                                                        \
       0                                                                                      \
     }                                                                                        \
   }
 
-EntryUps g_entriesUps[] = {HFGUPS_ENTRY(0, 3), HFGUPS_ENTRY(1, 3), HFGUPS_ENTRY(0, 2),
-                           HFGUPS_ENTRY(1, 2)};
+// bf16x3 (NP 3, bf16), f16x3 (NP 3, f16), bf16w (NP 2 on the f16 kernel)
+EntryUps g_entriesUps[] = {HFGUPS_ENTRY(0, 3, 0), HFGUPS_ENTRY(1, 3, 0), HFGUPS_ENTRY(0, 3, 1),
+                           HFGUPS_ENTRY(1, 3, 1), HFGUPS_ENTRY(0, 2, 1), HFGUPS_ENTRY(1, 2, 1)};
 
 }  // namespace
 
@@ -385,11 +405,11 @@ size_t ups_lds_bytes(int cfg) {
   return 2 * slab + 2 * 2 * xr * 32;
 }
 
-hipError_t launch_ups_bf16x3(int cfg, int np, const UpsParams& p, hipStream_t stream,
+hipError_t launch_ups_bf16x3(int cfg, int fmt, int np, const UpsParams& p, hipStream_t stream,
                              const char** name) {
   EntryUps* e = nullptr;
   for (auto& cand : g_entriesUps)
-    if (cand.cfg == cfg && cand.np == np) e = &cand;
+    if (cand.cfg == cfg && cand.np == np && cand.fmt == fmt) e = &cand;
   if (!e) return hipErrorInvalidValue;
   const UpsCfg& t = kUpsCfgs[cfg];
   // shapes the kernel's indexing assumes
@@ -400,8 +420,8 @@ hipError_t launch_ups_bf16x3(int cfg, int np, const UpsParams& p, hipStream_t st
   {
     std::lock_guard<std::mutex> lk(setup_mutex());
     if (!e->name[0])
-      snprintf(e->name, sizeof(e->name), "ups_bf16x3<%d, %d, %d, %d, %d>", t.WAVES_M, t.WAVES_N,
-               t.WM, t.WN, np);
+      snprintf(e->name, sizeof(e->name), "ups_bf16x3<%d, %d, %d, %d, %d, %d>", t.WAVES_M,
+               t.WAVES_N, t.WM, t.WN, np, fmt);
   }
   const size_t lds = ups_lds_bytes(cfg);
   if (lds > 160 * 1024) return hipErrorInvalidValue;

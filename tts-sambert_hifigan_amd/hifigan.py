@@ -60,13 +60,17 @@ def _lengths_on(lengths, device) -> torch.Tensor:
     return host.to(device, non_blocking=True)
 
 
+PRECISIONS = ("f16x3", "fp32", "bf16x3", "bf16w")
+
+
 def default_precision() -> str:
-    """The precision a module gets when its constructor is not given one: "fp32" (exact),
-    or ``HFG_PRECISION`` from the environment ("fp32", "bf16x3", "bf16w"), so a reference
-    code base can switch its Generator to the split-precision path without code changes."""
-    p = os.environ.get("HFG_PRECISION", "fp32")
-    if p not in ("fp32", "bf16x3", "bf16w"):
-        raise ValueError(f"HFG_PRECISION={p!r}: expected fp32, bf16x3 or bf16w")
+    """The precision a module gets when its constructor is not given one: "f16x3"
+    (fp32-class split products on the f16 matrix cores, include/hifigan_hip.h), or
+    ``HFG_PRECISION`` from the environment ("f16x3", "fp32", "bf16x3", "bf16w"), so a
+    reference code base can switch its Generator's arithmetic without code changes."""
+    p = os.environ.get("HFG_PRECISION", "f16x3")
+    if p not in PRECISIONS:
+        raise ValueError(f"HFG_PRECISION={p!r}: expected one of {', '.join(PRECISIONS)}")
     return p
 
 
