@@ -118,15 +118,19 @@ def parse():
     ap.add_argument("--preset", default="v1", choices=["v1", "v2star"])
     ap.add_argument("--batch", type=int, default=8, help="utterances per GPU")
     ap.add_argument("--frames", type=int, default=1024)
-    ap.add_argument("--precision", default="bf16x3", choices=["fp32", "f16x3", "bf16x3", "bf16w"],
-                    help="conv arithmetic: bf16x3 split-precision MFMA (default; parity 1e-4 "
-                         "met, tests/test_gpu_parity.py), exact fp32 MFMA, or bf16w (weights "
-                         "stored as bf16: a different model, parity against the bf16-rounded "
-                         "weights, tests/test_gpu_bf16w.py)")
-    ap.add_argument("--also", nargs="*", default=["fp32", "bf16w"],
+    ap.add_argument("--precision", default="f16x3", choices=["fp32", "f16x3", "bf16x3", "bf16w"],
+                    help="conv arithmetic: f16x3 split-precision MFMA (default: scaled f16 "
+                         "halves, fp32-class products, every golden fixture within the exact-fp32 "
+                         "bars, tests/test_gpu_stages.py), bf16x3 (bf16 halves: faster, ~16-bit "
+                         "products), exact fp32 MFMA, or bf16w (weights stored as bf16: a "
+                         "different model, parity against the bf16-rounded weights)")
+    ap.add_argument("--also", nargs="*", default=["bf16x3", "fp32", "bf16w"],
                     help="extra precisions measured in the same run (reported under 'alt')")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl = RCCL over xGMI (production); gloo only to rehearse N>1 on one GPU")
+    ap.add_argument("--force-dist", action="store_true",
+                    help="initialise the process group (and broadcast the weights) even at N = 1: "
+                         "exercises the RCCL branch on a one-GPU box")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extra", action="store_true",
                     help="skip the other BASELINE configs (C1 latency + hipGraph, C4 V2*, C5 ragged)")
@@ -476,7 +480,8 @@ def main():
     dev_index = local_rank % torch.cuda.device_count()
     torch.cuda.set_device(dev_index)
     dev = torch.device("cuda", dev_index)
-    if world > 1:
+    use_dist = world > 1 or args.force_dist
+    if use_dist:
         if args.dist_backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
         else:
@@ -497,7 +502,7 @@ def main():
     spec = [(k, s) for k, s, _ in S.param_specs(cfg)]
     sd_np = S.random_state_dict(cfg, seed=0) if rank == 0 else None
     coll_dev = dev if args.dist_backend == "nccl" else torch.device("cpu")
-    if world > 1:
+    if use_dist:
         sd = hdist.broadcast_state_dict({k: torch.from_numpy(v) for k, v in sd_np.items()}
                                         if rank == 0 else None, spec, coll_dev, src=0)
     else:
@@ -540,7 +545,7 @@ def main():
             h.profile_reset()
             h.set_profiling(True)
         evs = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
-        if world > 1:
+        if use_dist:
             dist.barrier()
         torch.cuda.synchronize(dev)
         t0 = time.perf_counter()
@@ -553,7 +558,7 @@ def main():
         step_ms = sorted(evs[i].elapsed_time(evs[i + 1]) for i in range(args.steps))
         ev_median[precision] = step_ms[len(step_ms) // 2] if len(step_ms) % 2 else \
             0.5 * (step_ms[len(step_ms) // 2 - 1] + step_ms[len(step_ms) // 2])
-        if world > 1:
+        if use_dist:
             dist.barrier()
             t = torch.zeros(world, dtype=torch.float64, device=coll_dev)
             t[rank] = elapsed
@@ -628,7 +633,7 @@ def main():
     ms_per_step = 1000.0 * elapsed / args.steps
 
     if rank != 0:
-        if world > 1:
+        if use_dist:
             dist.destroy_process_group()
         return
 
@@ -660,10 +665,10 @@ def main():
         },
         "value_per_gpu": value / world,
         "per_rank_ms_per_step": rank_ms.get(args.precision),
-        "world_size_observed": dist.get_world_size() if world > 1 else 1,
-        "dist_backend": args.dist_backend if world > 1 else None,
+        "world_size_observed": dist.get_world_size() if use_dist else 1,
+        "dist_backend": args.dist_backend if use_dist else None,
         "launch": ("self-launched torch.distributed.run" if os.environ.get("HFG_BENCH_SELF_LAUNCHED")
-                   else "external launcher" if world > 1 else "single process"),
+                   else "external launcher" if "RANK" in os.environ else "single process"),
         "value_note": "value = whole-job aggregate (all ranks' samples / max-over-ranks time, the "
                       "bench contract); value_per_gpu = value / n_gpus",
         "rtf": (elapsed / args.steps) / (args.batch * out_len / SAMPLE_RATE),
@@ -801,7 +806,7 @@ def main():
         line["cpu_baseline"] = cpu_baseline(cfg, cfg_np, T, args.cpu_budget_s)
         line["cpu_baseline"]["gpu_over_cpu"] = value / line["cpu_baseline"]["value"]
     print(json.dumps(line), flush=True)
-    if world > 1:
+    if use_dist:
         dist.destroy_process_group()
 
 

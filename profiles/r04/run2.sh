@@ -7,7 +7,7 @@ timeout -k 10 120 python -u tests/tools/probe_rates.py > gpurun_out/r04/probe2.j
 rc=$?; echo "probe rc=$rc"; if [ $rc -ne 0 ]; then exit $rc; fi
 timeout -k 10 900 python -u -m pytest -v --timeout 300 --timeout-method thread \
   tests/test_gpu_parity.py tests/test_gpu_stages.py tests/test_gpu_latency_paths.py \
-  tests/test_gpu_bf16w.py > gpurun_out/r04/t2.log 2>&1
+  tests/test_gpu_bf16w.py tests/test_gpu_dist.py > gpurun_out/r04/t2.log 2>&1
 rc=$?
 echo "pytest rc=$rc"
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi

@@ -65,6 +65,48 @@ def test_world2_vocode_sharded_bitwise(dev):
             assert chk["max_err_vs_reference_wav"] < 1e-4, name
 
 
+def test_nccl_world1_vocode_sharded_bitwise(dev):
+    """The RCCL branch on the one-GPU box: one rank under
+    torch.distributed.run, backend nccl, device_id set — the weight broadcast and
+    vocode_sharded's batch broadcast (src=0) on device buffers, each wav bitwise the
+    single-process forward.  Point-to-point sends need two GPUs: left to the 8-GPU run."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1",
+           "--master-addr", "127.0.0.1", "--master-port", str(_port()),
+           os.path.join(ROOT, "tests", "tools", "dist_world2_check.py")]
+    env = dict(os.environ, HFG_DIST_BACKEND="nccl")
+    r = subprocess.run(["timeout", "-k", "10", "240"] + cmd, cwd=ROOT, capture_output=True,
+                       text=True, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    res = _last_json(r.stdout)
+    print("\n" + json.dumps(res, indent=1))
+    assert res["world"] == 1 and res["backend"] == "nccl"
+    assert res["weights_on"].startswith("cuda")
+    assert set(res["checks"]) == {"C3_v1_64x80x1024/f16x3", "C5_sambert_b32/f16x3",
+                                  "C5_sambert_b32/fp32"}
+    for name, chk in res["checks"].items():
+        assert chk["bitwise_vs_single_process"], name
+        if "max_err_vs_reference_wav" in chk:
+            assert chk["max_err_vs_reference_wav"] < 1e-4, name
+
+
+def test_bench_gpus1_nccl(dev):
+    """bench.py --dist-backend nccl --force-dist at N = 1: the bench's RCCL branch
+    (init_process_group("nccl", device_id=...), the flat weight broadcast on the GPU) runs
+    and reports world size 1."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1",
+           "--master-addr", "127.0.0.1", "--master-port", str(_port()),
+           os.path.join(ROOT, "bench.py"), "--gpus", "1", "--dist-backend", "nccl", "--force-dist",
+           "--steps", "2", "--warmup", "1", "--no-extra", "--no-cpu-baseline", "--no-pmc", "--also"]
+    r = subprocess.run(["timeout", "-k", "10", "300"] + cmd, cwd=ROOT, capture_output=True,
+                       text=True)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = _last_json(r.stdout)
+    print("\n" + json.dumps({k: line.get(k) for k in ("n_gpus", "value", "world_size_observed",
+                                                       "dist_backend", "launch")}))
+    assert line["n_gpus"] == 1 and line["world_size_observed"] == 1
+    assert line["dist_backend"] == "nccl"
+
+
 def test_bench_gpus2_self_launch(dev):
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dist-backend", "gloo",
            "--steps", "2", "--warmup", "1", "--no-extra", "--no-cpu-baseline", "--no-pmc",

@@ -10,7 +10,8 @@ pytestmark = pytest.mark.gpu
 
 
 @pytest.mark.parametrize("kind,lo,hi", [(0, 300.0, 2500.0 * 1.02), (1, 40.0, 157.3 * 1.02),
-                                         (2, 100.0, 2500.0 * 1.02), (3, 10.0, 157.3 * 1.02)])
+                                         (2, 100.0, 2500.0 * 1.02), (3, 10.0, 157.3 * 1.02),
+                                         (4, 300.0, 2500.0 * 1.02), (5, 100.0, 2500.0 * 1.02)])
 def test_probe_mfma_rate_plausible(pkg, kind, lo, hi):
     if not torch.cuda.is_available():
         pytest.skip("no HIP device")
@@ -20,4 +21,4 @@ def test_probe_mfma_rate_plausible(pkg, kind, lo, hi):
     print(f"\nkind {kind}: {tf.value:.1f} TFLOP/s dense at {mhz.value:.0f} MHz")
     assert lo < tf.value < hi
     assert 500.0 < mhz.value < 2600.0
-    assert lib.hfg_probe_mfma_rate(0, 4, 10, ctypes.byref(tf), ctypes.byref(mhz)) == -22
+    assert lib.hfg_probe_mfma_rate(0, 6, 10, ctypes.byref(tf), ctypes.byref(mhz)) == -22

@@ -180,10 +180,17 @@ def test_profiling_summary(pkg, v1, dev):
     run(gen, torch.randn(1, 80, 64, device=dev))
     h.set_profiling(False)
     prof = h.profile_summary()
-    # 78 conv launches; a small forward runs its MRFs' ResBlocks on concurrent streams and
-    # adds one mrf_combine launch per such stage (hifigan_capi.cpp run_mrf)
+    # the default (f16x3) schedule: conv_pre, 4 upsamplers, conv_post, the stage-0 and stage-1
+    # k = 7 / 11 ResBlocks layer by layer (6 launches each), the other ResBlocks one whole-
+    # ResBlock launch each (two for the split k = 11 ones at C = 32 / 64); a small forward
+    # runs its MRFs' ResBlocks on concurrent streams and adds one mrf_combine launch per such
+    # stage (hifigan_capi.cpp run_mrf); the mel's scale slot comes from one absmax launch
+    assert gen.precision == "f16x3"
     combine = prof.get("mrf_combine", {"launches": 0})["launches"]
-    assert sum(v["launches"] for v in prof.values()) - combine == 78
+    assert prof.get("absmax", {"launches": 0})["launches"] == 1, sorted(prof)
+    n_conv = sum(v["launches"] for k, v in prof.items() if k not in ("mrf_combine", "absmax"))
+    # 6 (pre, ups x4, post) + stage 0: 3 x 6 + stage 1: 2 x 6 + 1 + stages 2, 3: 1 + 1 + 2 each
+    assert n_conv == 6 + 3 * 6 + 2 * 6 + 1 + 4 + 4, sorted(prof.items())
     assert combine <= 4
     assert all(v["ms"] > 0 for k, v in prof.items() if k != "mrf_combine")
     from oracle import config as C

@@ -39,7 +39,9 @@ def test_mel_handle_host_only(pkg):
     c = _cfg(pkg)
     assert lib.hfg_mel_create(ctypes.byref(c), -1, ctypes.byref(h)) == 0
     assert lib.hfg_mel_frames(h, 22050) == 22050 // 256 + 1
-    assert lib.hfg_mel_workspace_bytes(h, 2, 22050) == 4 * 2 * 87 * 513
+    # n_fft 1024 (a power of two): the one-launch FFT path, spectra in LDS, a token
+    # workspace (the DFT path's B x frames x bins buffer is not allocated)
+    assert lib.hfg_mel_workspace_bytes(h, 2, 22050) == 256
     assert lib.hfg_mel_forward(h, None, 1, 22050, None, None, 0, None) == -22
     lib.hfg_mel_destroy(h)
     c.win_length = 2048

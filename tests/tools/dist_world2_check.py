@@ -10,6 +10,11 @@ rank 0, which compares them BITWISE with a single-process forward of the whole b
 C3 (V1 [64, 80, 1024]) and C5 (the reference SAM-BERT acoustic model's 32 ragged
 utterances, tests/golden/c5_sambert_b32.npz, also within 1e-4 of the reference wavs).
 Rank 0 prints one JSON line.  Used by tests/test_gpu_dist.py.
+
+HFG_DIST_BACKEND=nccl runs the same checks over RCCL (one rank per GPU: world size 1 on the
+one-GPU box): ``dist.init_process_group("nccl", device_id=...)``, the weight broadcast and the
+batch broadcast of ``vocode_sharded(..., src=0)`` on device buffers — the production path of
+``bench.py --gpus N`` and of an 8-GPU node, short of point-to-point sends between two GPUs.
 """
 import json
 import os
@@ -31,12 +36,18 @@ def main():
     hd = importlib.import_module(ge.PKG_NAME + ".dist")
     from oracle import config as C  # the checker's weights and fixtures
 
-    dist.init_process_group("gloo")
-    rank, world = dist.get_rank(), dist.get_world_size()
+    backend = os.environ.get("HFG_DIST_BACKEND", "gloo")
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dev = torch.device("cuda", local % torch.cuda.device_count())
     torch.cuda.set_device(dev)
-    res = {"world": world, "checks": {}}
+    if backend == "nccl":
+        dist.init_process_group("nccl", device_id=dev)
+    else:
+        dist.init_process_group("gloo")
+    rank, world = dist.get_rank(), dist.get_world_size()
+    # collective buffers: device memory for RCCL, host memory for gloo
+    cdev = dev if backend == "nccl" else torch.device("cpu")
+    res = {"world": world, "backend": dist.get_backend(), "checks": {}}
     gd = os.path.join(ROOT, "tests", "golden")
     meta = json.load(open(os.path.join(gd, "golden_c5.json")))
     arr = np.load(os.path.join(gd, "c5_sambert_b32.npz"))
@@ -45,7 +56,8 @@ def main():
         spec = [(k, s) for k, s, _ in C.param_specs(cfg)]
         sd0 = ({k: torch.from_numpy(v) for k, v in
                 C.make_state_dict(cfg, seed=meta["vocoder_seed"]).items()} if rank == 0 else None)
-        sd = hd.broadcast_state_dict(sd0, spec, torch.device("cpu"), src=0)
+        sd = hd.broadcast_state_dict(sd0, spec, cdev, src=0)
+        res["weights_on"] = str(next(iter(sd.values())).device)
         gen = pkg.HiFiGANGenerator(**cfg.kwargs(), precision=precision).eval()
         gen.load_state_dict(sd)
         gen = gen.to(dev)

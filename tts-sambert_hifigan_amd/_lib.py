@@ -201,15 +201,21 @@ def load_library(path: str = LIB_PATH):
             f"{path} is missing: the HIP extension must be built first "
             "(python tts-sambert_hifigan_amd/build.py). There is no CPU fallback.")
     lib = ctypes.CDLL(path)
+    # a library missing an entry point is stale: refuse it, unless the caller
+    # opts in for a same-box A/B against a previous commit's build (HFG_ALLOW_OLD_LIB=1)
+    allow_old = os.environ.get("HFG_ALLOW_OLD_LIB") == "1"
+    missing = []
     for name, (res, args) in SIGNATURES.items():
-        # an older build (a same-box A/B against a previous commit's library) may lack a
-        # newer entry point: it then fails when called; the build itself is checked to
-        # export every header symbol (tests/test_capi_host.py)
         fn = getattr(lib, name, None)
         if fn is None:
+            missing.append(name)
             continue
         fn.restype = res
         fn.argtypes = args
+    if missing and not allow_old:
+        raise HipExtensionMissing(
+            f"{path} lacks {', '.join(missing)}: it was built from an older tree; rebuild it "
+            "(python tts-sambert_hifigan_amd/build.py) or set HFG_ALLOW_OLD_LIB=1 for an A/B")
     _lib = lib
     return lib
 

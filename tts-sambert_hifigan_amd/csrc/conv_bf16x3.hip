@@ -642,14 +642,9 @@ conv1d_bf16x3(const ConvParams p) {
     if (acc[0][0][0] == 1.2345e-30f) p.y[0] = acc[WM - 1][WN - 1][15];
     return;
   }
-  if constexpr (FMT == kFmtF16) {
-    // products of 2^ex-scaled inputs and 2^ew-scaled weights: exact power-of-two unscale
-    const float inv = exp2i(-(ex + p.ew));
-#pragma unroll
-    for (int i = 0; i < WM; ++i)
-#pragma unroll
-      for (int k = 0; k < WN; ++k) acc[i][k] = acc[i][k] * inv;
-  }
+  // products of 2^ex-scaled inputs and 2^ew-scaled weights: the exact power-of-two unscale
+  // joins the bias add (fma(acc, sc, bias); bitwise acc + bias for sc = 1)
+  const float sc = FMT == kFmtF16 ? exp2i(-(ex + p.ew)) : 1.0f;
 
   // ---- epilogue (same contract as conv1d_mfma_f32) ----
   if constexpr (UPS) {
@@ -691,10 +686,10 @@ conv1d_bf16x3(const ConvParams p) {
             const int co = co_of(row);
             const int t = n * s_ + (row - co * s_) - p_;
             float4 v;
-            v.x = acc[i][k][4 * q + 0] + bv[4 * q + 0];
-            v.y = acc[i][k][4 * q + 1] + bv[4 * q + 1];
-            v.z = acc[i][k][4 * q + 2] + bv[4 * q + 2];
-            v.w = acc[i][k][4 * q + 3] + bv[4 * q + 3];
+            v.x = __builtin_fmaf(acc[i][k][4 * q + 0], sc, bv[4 * q + 0]);
+            v.y = __builtin_fmaf(acc[i][k][4 * q + 1], sc, bv[4 * q + 1]);
+            v.z = __builtin_fmaf(acc[i][k][4 * q + 2], sc, bv[4 * q + 2]);
+            v.w = __builtin_fmaf(acc[i][k][4 * q + 3], sc, bv[4 * q + 3]);
             *reinterpret_cast<float4*>(yb + (int64_t)co * p.L_out + t) = v;
             track4(v);
           }
@@ -709,10 +704,10 @@ conv1d_bf16x3(const ConvParams p) {
             const int co = co_of(row);
             const int t = n * s_ + (row - co * s_) - p_;
             float4 v;
-            v.x = acc[i][k][4 * q + 0] + bv[4 * q + 0];
-            v.y = acc[i][k][4 * q + 1] + bv[4 * q + 1];
-            v.z = acc[i][k][4 * q + 2] + bv[4 * q + 2];
-            v.w = acc[i][k][4 * q + 3] + bv[4 * q + 3];
+            v.x = __builtin_fmaf(acc[i][k][4 * q + 0], sc, bv[4 * q + 0]);
+            v.y = __builtin_fmaf(acc[i][k][4 * q + 1], sc, bv[4 * q + 1]);
+            v.z = __builtin_fmaf(acc[i][k][4 * q + 2], sc, bv[4 * q + 2]);
+            v.w = __builtin_fmaf(acc[i][k][4 * q + 3], sc, bv[4 * q + 3]);
             float* dst = yb + (int64_t)co * p.L_out + t;
             if (t >= 0 && t + 3 < L_out_b) {
               *reinterpret_cast<float4*>(dst) = v;
@@ -733,7 +728,7 @@ conv1d_bf16x3(const ConvParams p) {
           const int co = co_of(row);
           const int t = n * s_ + (row - co * s_) - p_;
           if (t >= 0 && t < L_out_b) {
-            const float v = acc[i][k][r] + bv[r];
+            const float v = __builtin_fmaf(acc[i][k][r], sc, bv[r]);
             yb[(int64_t)co * p.L_out + t] = v;
             vmax = fmaxf(vmax, fabsf(v));
           }
@@ -752,10 +747,10 @@ conv1d_bf16x3(const ConvParams p) {
       lds_barrier();
       float* stage = reinterpret_cast<float*>(lds16) + wave * 32 * (32 * WN + 8);
       conv_epilogue_lds<WM, WN>(p, acc, b, mt * MT + wave_m * 32 * WM, n0 + wave_n * 32 * WN,
-                                N_b, half, col, stage, lane);
+                                N_b, half, col, stage, lane, sc);
     } else {
       conv_epilogue<WM, WN>(p, acc, b, mt * MT + wave_m * 32 * WM, n0 + wave_n * 32 * WN, N_b,
-                            half, col);
+                            half, col, sc);
     }
   }
 }

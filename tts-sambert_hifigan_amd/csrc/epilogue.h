@@ -11,17 +11,34 @@
 
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "kernels.h"
 
 namespace hfg {
 
 typedef float floatx16e __attribute__((ext_vector_type(16)));
 
-// largest value over a wave's lanes
+// largest value over a wave (every lane active): DPP max within each 16-lane row (quad swaps,
+// then row rotations by 4 and 8), then the 4 row maxima by readlane — a few cycles per step,
+// where ds_bpermute shuffles put ~6 LDS round trips on the critical path
 __device__ __forceinline__ float wave_max(float m) {
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
-  return m;
+  auto step = [&](auto ctrl_tag) {
+    constexpr int CTRL = decltype(ctrl_tag)::value;
+    const float o = __builtin_bit_cast(
+        float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, m), CTRL, 0xF, 0xF, false));
+    m = fmaxf(m, o);
+  };
+  step(std::integral_constant<int, 0xB1>{});   // quad_perm [1,0,3,2]
+  step(std::integral_constant<int, 0x4E>{});   // quad_perm [2,3,0,1]
+  step(std::integral_constant<int, 0x124>{});  // row_ror:4
+  step(std::integral_constant<int, 0x128>{});  // row_ror:8
+  const int mi = __builtin_bit_cast(int, m);
+  const float r0 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(mi, 0));
+  const float r1 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(mi, 16));
+  const float r2 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(mi, 32));
+  const float r3 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(mi, 48));
+  return fmaxf(fmaxf(r0, r1), fmaxf(r2, r3));
 }
 // fold a lane's max |value| into item b's producer slot: one vector atomic per wave (the
 // slots are zeroed by the host before the forward; non-negative floats order like their bit
@@ -36,10 +53,13 @@ __device__ __forceinline__ void amax_commit(float m, uint32_t* slots, int b) {
   if ((threadIdx.x & 63) == 0) atomicMax(slot, __builtin_bit_cast(uint32_t, m));
 }
 
+// sc: the accumulator's scale (f16x3: 2^-(e_x + e_w); 1 otherwise): v = fma(acc, sc, bias),
+// bitwise acc + bias for sc = 1
 template <int WM, int WN>
 __device__ __forceinline__ void conv_epilogue(const ConvParams& p, const float* __restrict__ bias,
                                               floatx16e (&acc)[WM][WN], int b, int row_base,
-                                              int n_base, int N_b, int half, int col) {
+                                              int n_base, int N_b, int half, int col,
+                                              float sc = 1.0f) {
   const int64_t bo = (int64_t)b * p.y_bs;
   const char* resb = p.res ? reinterpret_cast<const char*>(p.res + bo) : nullptr;
   char* outb = reinterpret_cast<char*>((p.mrf ? p.mrf : p.y) + bo);
@@ -70,7 +90,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvParams& p, const float* 
         const int row = row_base + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
         ok[r] = nok && row < p.M;
         off[r] = ok[r] ? (unsigned)(row * p.N + n) * 4u : 0u;
-        v[r] = acc[i][k][r] + bv[r];
+        v[r] = __builtin_fmaf(acc[i][k][r], sc, bv[r]);
       }
       if (resb) {
         float rv[16];
@@ -114,8 +134,8 @@ __device__ __forceinline__ void conv_epilogue(const ConvParams& p, const float* 
 template <int WM, int WN>
 __device__ __forceinline__ void conv_epilogue(const ConvParams& p, floatx16e (&acc)[WM][WN],
                                               int b, int row_base, int n_base, int N_b,
-                                              int half, int col) {
-  conv_epilogue<WM, WN>(p, p.bias, acc, b, row_base, n_base, N_b, half, col);
+                                              int half, int col, float sc = 1.0f) {
+  conv_epilogue<WM, WN>(p, p.bias, acc, b, row_base, n_base, N_b, half, col, sc);
 }
 
 // The same contract with the tile staged through LDS: each wave writes 32 accumulator
@@ -129,7 +149,8 @@ __device__ __forceinline__ void conv_epilogue(const ConvParams& p, floatx16e (&a
 template <int WM, int WN>
 __device__ __forceinline__ void conv_epilogue_lds(const ConvParams& p, floatx16e (&acc)[WM][WN],
                                                   int b, int row_base, int n_base, int N_b,
-                                                  int half, int col, float* stage, int lane) {
+                                                  int half, int col, float* stage, int lane,
+                                                  float sc = 1.0f) {
   constexpr int SROW = 32 * WN + 8;
   constexpr int C4 = 8 * WN;                 // float4 per staged row
   const int64_t bo = (int64_t)b * p.y_bs;
@@ -188,10 +209,10 @@ __device__ __forceinline__ void conv_epilogue_lds(const ConvParams& p, floatx16e
         full[u] = ok[u] && n[u] + 3 < N_b;
         v[u] = *reinterpret_cast<const float4*>(stage + rr * SROW + 4 * c4);
         const float bv = p.bias[row[u]];
-        v[u].x += bv;
-        v[u].y += bv;
-        v[u].z += bv;
-        v[u].w += bv;
+        v[u].x = __builtin_fmaf(v[u].x, sc, bv);
+        v[u].y = __builtin_fmaf(v[u].y, sc, bv);
+        v[u].z = __builtin_fmaf(v[u].z, sc, bv);
+        v[u].w = __builtin_fmaf(v[u].w, sc, bv);
       }
       if (resb) {
 #pragma unroll
@@ -235,11 +256,15 @@ __device__ __forceinline__ void conv_epilogue_lds(const ConvParams& p, floatx16e
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
           // the stored elements only: a partial quad's tail past N_b is not written
-          const int nv = ok[u] ? min(N_b - n[u], 4) : 0;
-          vmax = nv > 0 ? fmaxf(vmax, fabsf(v[u].x)) : vmax;
-          vmax = nv > 1 ? fmaxf(vmax, fabsf(v[u].y)) : vmax;
-          vmax = nv > 2 ? fmaxf(vmax, fabsf(v[u].z)) : vmax;
-          vmax = nv > 3 ? fmaxf(vmax, fabsf(v[u].w)) : vmax;
+          if (full[u]) {
+            vmax = fmaxf(vmax, fmaxf(fmaxf(fabsf(v[u].x), fabsf(v[u].y)),
+                                     fmaxf(fabsf(v[u].z), fabsf(v[u].w))));
+          } else if (ok[u]) {
+            const int nv = N_b - n[u];
+            vmax = fmaxf(vmax, fabsf(v[u].x));
+            if (nv > 1) vmax = fmaxf(vmax, fabsf(v[u].y));
+            if (nv > 2) vmax = fmaxf(vmax, fabsf(v[u].z));
+          }
         }
       }
 #pragma unroll

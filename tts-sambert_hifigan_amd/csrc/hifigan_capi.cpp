@@ -1499,8 +1499,10 @@ int forward_impl(hfg_handle* h, const float* mel, int64_t B, int64_t T, const hf
   // f16x3: the mel's per-item max |value| (no kernel produced it)
   uint32_t* a_mel = ln.take();
   if (a_mel) {
+    ln.begin(0.0, 4.0 * B * c.n_mels * T);
     hipError_t e = hfg::launch_absmax(mel, (int64_t)c.n_mels * T, btc ? 1 : T, btc ? c.n_mels : 1,
                                       c.n_mels, (int)T, lens_at(0), (int)B, a_mel, stream);
+    ln.end("absmax");
     if (e != hipSuccess) return fail(HFG_EIO, "launch absmax: %s", hipGetErrorString(e));
   }
   // conv_pre  (models/hifigan.py:238)

@@ -114,22 +114,42 @@ int upload_tables(hfg_mel_handle* h, const float* win, const float* fb) {
   int prev = -1;
   (void)hipGetDevice(&prev);
   if (hipSetDevice(h->device) != hipSuccess) return mfail(HFG_ENODEV, "hipSetDevice(%d)", h->device);
-  auto put = [&](void** dst, const void* src, size_t bytes) -> bool {
-    if (*dst) (void)hipFree(*dst);
-    *dst = nullptr;
-    if (hipMalloc(dst, bytes) != hipSuccess) return false;
-    return hipMemcpy(*dst, src, bytes, hipMemcpyHostToDevice) == hipSuccess;
+  // every new table is allocated and filled before any old one is released: a failure leaves
+  // the handle's previous (complete) tables in place
+  struct Tbl {
+    void** dst;
+    const void* src;
+    size_t bytes;
+    void* fresh;
   };
-  bool ok = true;
+  std::vector<Tbl> tbls;
   if (!h->fft) {
-    ok = ok && put(reinterpret_cast<void**>(&h->tcos), tc.data(), tc.size() * 4);
-    ok = ok && put(reinterpret_cast<void**>(&h->tsin), ts.data(), ts.size() * 4);
-    ok = ok && put(reinterpret_cast<void**>(&h->fb), fb, h->fb_host.size() * 4);
+    tbls.push_back({reinterpret_cast<void**>(&h->tcos), tc.data(), tc.size() * 4, nullptr});
+    tbls.push_back({reinterpret_cast<void**>(&h->tsin), ts.data(), ts.size() * 4, nullptr});
+    tbls.push_back({reinterpret_cast<void**>(&h->fb), fb, h->fb_host.size() * 4, nullptr});
   }
-  ok = ok && put(reinterpret_cast<void**>(&h->win), win, (size_t)N * 4);
-  ok = ok && put(&h->tw, tw_h.data(), tw_h.size() * 8);
-  ok = ok && put(reinterpret_cast<void**>(&h->band), band_h.data(), band_h.size() * 4);
-  ok = ok && put(reinterpret_cast<void**>(&h->bw), bw_h.data(), bw_h.size() * 4);
+  tbls.push_back({reinterpret_cast<void**>(&h->win), win, (size_t)N * 4, nullptr});
+  tbls.push_back({&h->tw, tw_h.data(), tw_h.size() * 8, nullptr});
+  tbls.push_back({reinterpret_cast<void**>(&h->band), band_h.data(), band_h.size() * 4, nullptr});
+  tbls.push_back({reinterpret_cast<void**>(&h->bw), bw_h.data(), bw_h.size() * 4, nullptr});
+  bool ok = true;
+  for (auto& t : tbls) {
+    ok = hipMalloc(&t.fresh, t.bytes) == hipSuccess &&
+         hipMemcpy(t.fresh, t.src, t.bytes, hipMemcpyHostToDevice) == hipSuccess;
+    if (!ok) break;
+  }
+  if (ok) {
+    // a forward in flight may still read the old tables
+    ok = hipDeviceSynchronize() == hipSuccess;
+  }
+  for (auto& t : tbls) {
+    if (ok) {
+      if (*t.dst) (void)hipFree(*t.dst);
+      *t.dst = t.fresh;
+    } else if (t.fresh) {
+      (void)hipFree(t.fresh);
+    }
+  }
   if (prev >= 0) (void)hipSetDevice(prev);
   return ok ? HFG_OK : mfail(HFG_ENOMEM, "mel tables: device allocation / copy failed");
 }
@@ -236,12 +256,15 @@ int64_t hfg_mel_frames(const hfg_mel_handle* h, int64_t n_samples) {
 
 size_t hfg_mel_workspace_bytes(const hfg_mel_handle* h, int64_t B, int64_t n_samples) {
   if (!h || B <= 0 || n_samples <= 0) return 0;
+  // the one-launch FFT path keeps its spectra in LDS: no workspace (a token 256 B, so callers
+  // that allocate what this returns hold a valid pointer)
+  if (h->fft) return 256;
   return sizeof(float) * (size_t)B * (size_t)hfg_mel_frames(h, n_samples) * (size_t)h->n_bins;
 }
 
 int hfg_mel_forward(hfg_mel_handle* h, const float* wav, int64_t B, int64_t n_samples, float* mel,
                     void* workspace, size_t workspace_bytes, void* stream) {
-  if (!h || !wav || !mel || !workspace) return mfail(HFG_EINVAL, "NULL argument");
+  if (!h || !wav || !mel || (!workspace && !h->fft)) return mfail(HFG_EINVAL, "NULL argument");
   if (h->device < 0) return mfail(HFG_EINVAL, "host-only mel handle");
   if (B <= 0) return mfail(HFG_EINVAL, "B must be > 0");
   if (n_samples <= h->cfg.n_fft / 2)

@@ -199,9 +199,10 @@ resblock_bf16x3(const RbParams p) {
 #pragma unroll
     for (int k = 0; k < WN; ++k) {
       const int c = cbase + 32 * k + col;
-      const bool ex_k = vk[k] && c >= radius && c < NWIN - radius;
+      float mk = 0.f;  // v_max3 over the column's 16 rows, one select per column
 #pragma unroll
-      for (int r = 0; r < 16; ++r) m = ex_k ? fmaxf(m, fabsf(v[k][r])) : m;
+      for (int r = 0; r < 16; ++r) mk = fmaxf(mk, fabsf(v[k][r]));
+      m = (vk[k] && c >= radius && c < NWIN - radius) ? fmaxf(m, mk) : m;
     }
     m = wave_max(m);
     if (lane == 0) amax_s[wave] = m;
@@ -395,9 +396,12 @@ resblock_bf16x3(const RbParams p) {
   if (p.amax_out) {  // f16x3 consumers of the stage output (block-uniform branch)
     float m = 0.f;
 #pragma unroll
-    for (int k = 0; k < WN; ++k)
+    for (int k = 0; k < WN; ++k) {
+      float mk = 0.f;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) m = ok[k] ? fmaxf(m, fabsf(xcur[k][r])) : m;
+      for (int r = 0; r < 16; ++r) mk = fmaxf(mk, fabsf(xcur[k][r]));
+      m = ok[k] ? fmaxf(m, mk) : m;
+    }
     amax_commit(m, p.amax_out, b);
   }
 }

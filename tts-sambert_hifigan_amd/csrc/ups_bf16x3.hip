@@ -253,15 +253,8 @@ ups_bf16x3(const UpsParams p) {
     lds_barrier();
   }
 
-  if constexpr (FMT == kFmtF16) {
-    const float inv = exp2i(-(ex + p.ew));
-#pragma unroll
-    for (int c = 0; c < 2; ++c)
-#pragma unroll
-      for (int i = 0; i < WM; ++i)
-#pragma unroll
-        for (int k = 0; k < WN; ++k) acc[c][i][k] = acc[c][i][k] * inv;
-  }
+  // f16x3: the exact power-of-two unscale joins the bias add (fma; bitwise acc + bias at 1)
+  const float sc = FMT == kFmtF16 ? exp2i(-(ex + p.ew)) : 1.0f;
 
   // ---- epilogue: bias, stores of whole sample runs ----
   float* yb = p.y + (int64_t)b * p.y_bs;
@@ -287,8 +280,10 @@ ups_bf16x3(const UpsParams p) {
         for (int r = 0; r < 16; r += 2) {
           const int co0 = rb + (r & 3) + 8 * (r >> 2);
           const float b0 = p.bias[co0], b1 = p.bias[co0 + 1];
-          const float l0 = acc[0][i][k][r] + b0, r0 = acc[1][i][k][r] + b0;
-          const float l1 = acc[0][i][k][r + 1] + b1, r1 = acc[1][i][k][r + 1] + b1;
+          const float l0 = __builtin_fmaf(acc[0][i][k][r], sc, b0);
+          const float r0 = __builtin_fmaf(acc[1][i][k][r], sc, b0);
+          const float l1 = __builtin_fmaf(acc[0][i][k][r + 1], sc, b1);
+          const float r1 = __builtin_fmaf(acc[1][i][k][r + 1], sc, b1);
           const float s0 = odd ? l0 : l1, s1 = odd ? r0 : r1;
           const float v0 = __builtin_bit_cast(
               float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, s0), 0xB1, 0xF, 0xF, false));
@@ -324,8 +319,8 @@ ups_bf16x3(const UpsParams p) {
           const int co = rb + (r & 3) + 8 * (r >> 2);
           const float bv = p.bias[co];
           floatx2 v;
-          v[0] = acc[0][i][k][r] + bv;
-          v[1] = acc[1][i][k][r] + bv;
+          v[0] = __builtin_fmaf(acc[0][i][k][r], sc, bv);
+          v[1] = __builtin_fmaf(acc[1][i][k][r], sc, bv);
           *reinterpret_cast<floatx2*>(yb + (int64_t)co * p.L_out + 2 * m) = v;
           t2(v[0], v[1]);
         }
@@ -339,10 +334,10 @@ ups_bf16x3(const UpsParams p) {
             const int co = (rb + 8 * q + 2 * pr) >> 1;
             const float bv = p.bias[co];
             float4 v;
-            v.x = acc[0][i][k][r0] + bv;
-            v.y = acc[0][i][k][r0 + 1] + bv;
-            v.z = acc[1][i][k][r0] + bv;
-            v.w = acc[1][i][k][r0 + 1] + bv;
+            v.x = __builtin_fmaf(acc[0][i][k][r0], sc, bv);
+            v.y = __builtin_fmaf(acc[0][i][k][r0 + 1], sc, bv);
+            v.z = __builtin_fmaf(acc[1][i][k][r0], sc, bv);
+            v.w = __builtin_fmaf(acc[1][i][k][r0 + 1], sc, bv);
             *reinterpret_cast<float4*>(yb + (int64_t)co * p.L_out + 4 * m) = v;
             t2(v.x, v.y);
             t2(v.z, v.w);
@@ -357,10 +352,10 @@ ups_bf16x3(const UpsParams p) {
 #pragma unroll
           for (int c = 0; c < 2; ++c) {
             float4 v;
-            v.x = acc[c][i][k][4 * q + 0] + bv;
-            v.y = acc[c][i][k][4 * q + 1] + bv;
-            v.z = acc[c][i][k][4 * q + 2] + bv;
-            v.w = acc[c][i][k][4 * q + 3] + bv;
+            v.x = __builtin_fmaf(acc[c][i][k][4 * q + 0], sc, bv);
+            v.y = __builtin_fmaf(acc[c][i][k][4 * q + 1], sc, bv);
+            v.z = __builtin_fmaf(acc[c][i][k][4 * q + 2], sc, bv);
+            v.w = __builtin_fmaf(acc[c][i][k][4 * q + 3], sc, bv);
             *reinterpret_cast<float4*>(yb + (int64_t)co * p.L_out + m * p.u + c * h + sp) = v;
             t2(v.x, v.y);
             t2(v.z, v.w);

@@ -128,7 +128,12 @@ class MelSpectrogram:
         self._fb = melscale_fbanks(n_fft // 2 + 1, float(f_min), float(f_max), n_mels,
                                    sample_rate, norm, mel_scale).contiguous()
         fp = ctypes.POINTER(ctypes.c_float)
-        if not hasattr(self.lib, "hfg_mel_set_tables"):  # an older library (A/B runs)
+        if not hasattr(self.lib, "hfg_mel_set_tables"):
+            # only an A/B against an older library (HFG_ALLOW_OLD_LIB=1) gets here: its
+            # device tables are double-evaluated, not torchaudio's float32 ones
+            import warnings
+            warnings.warn("libhifigan_hip.so lacks hfg_mel_set_tables: mel tables are "
+                          "double-evaluated, not the reference's float32 window / filterbank")
             return
         _check_mel(self.lib, self.lib.hfg_mel_set_tables(
             self.ptr, ctypes.cast(self._window.data_ptr(), fp), ctypes.cast(self._fb.data_ptr(), fp)))
