@@ -537,30 +537,29 @@ hipError_t launch_mrf_combine(const MrfCombineArgs& a, int batch, hipStream_t st
   return hipGetLastError();
 }
 
-// max |x| per item over its valid columns, folded into out[b] (one atomic per wave)
+// max |x| per item over its valid columns, folded into out[b] (one atomic per wave).  The
+// item is walked as rows of its contiguous dimension: channels x [0, len) for [C][T]
+// (x_ts == 1), frames [0, len) x channels for [T][C] (x_cs == 1) — no per-element division.
 __global__ void __launch_bounds__(256)
 absmax_kernel(const float* __restrict__ x, int64_t x_bs, int64_t x_cs, int64_t x_ts, int C, int L,
               const int32_t* __restrict__ len, uint32_t* __restrict__ out) {
   const int b = blockIdx.y;
   const int len_b = len ? min(max(len[b], 0), L) : L;
   const float* xb = x + (int64_t)b * x_bs;
-  const int64_t n = (int64_t)C * len_b;
+  const bool tc = x_ts == 1;  // [C][T]: rows = channels
+  const int rows = tc ? C : len_b, row_len = tc ? len_b : C;
+  const int64_t rs = tc ? x_cs : x_ts;
   float m = 0.f;
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
-    // element i of the item in (time-major for x_ts == 1 ? channel-major) order
-    const int64_t c = x_ts == 1 ? i / len_b : i % C;
-    const int64_t t = x_ts == 1 ? i % len_b : i / C;
-    m = fmaxf(m, fabsf(xb[c * x_cs + t * x_ts]));
-  }
+  for (int r = blockIdx.x; r < rows; r += gridDim.x)
+    for (int i = threadIdx.x; i < row_len; i += 256) m = fmaxf(m, fabsf(xb[r * rs + i]));
   amax_commit(m, out, b);
 }
 
 hipError_t launch_absmax(const float* x, int64_t x_bs, int64_t x_cs, int64_t x_ts, int C, int L,
                          const int32_t* len, int batch, uint32_t* out, hipStream_t stream) {
-  const int64_t n = (int64_t)C * L;
-  const int gx = (int)std::min<int64_t>((n + 256 * 16 - 1) / (256 * 16), 1024);
-  absmax_kernel<<<dim3(gx > 0 ? gx : 1, batch), dim3(256), 0, stream>>>(x, x_bs, x_cs, x_ts, C, L,
-                                                                       len, out);
+  const int rows = x_ts == 1 ? C : L;
+  const int gx = rows < 256 ? (rows > 0 ? rows : 1) : 256;
+  absmax_kernel<<<dim3(gx, batch), dim3(256), 0, stream>>>(x, x_bs, x_cs, x_ts, C, L, len, out);
   return hipGetLastError();
 }
 

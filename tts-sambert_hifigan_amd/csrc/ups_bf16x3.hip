@@ -157,17 +157,51 @@ ups_bf16x3(const UpsParams p) {
       xv[e] = __builtin_bit_cast(
           f4, __builtin_amdgcn_raw_buffer_load_b128(xrs, (int)xoff_lane, e * xcs4, 0));
   };
+  // The 8 lanes of a ds_write_b128 lane group hold 8 consecutive quads xq; writing frame tt
+  // of each quad at once put them on 2 of the 8 16-B bank groups (the row offset mod 128 B is
+  // tt * 32 + the half swizzle): a 4-way conflict (SQ: 1.2 / 1.49 bank-conflict cycles per
+  // LDS-active cycle).  HFG_UPS_ROT: lane xq writes its frames in the order
+  // tt = (j + g) & 3, g = (xq & 1) + ((xq >> 1) & 2) — with the swizzle bit (xq >> 1) & 1 the
+  // 8 lanes then cover all 8 bank groups (profiles/r04 bank model) — and the frames are
+  // rotated in registers by g first (2 selects per value); the layout and the readers are
+  // unchanged.
+#ifndef HFG_UPS_ROT
+#define HFG_UPS_ROT 1
+#endif
   auto store_x = [&](int buf) {
     if (!has_task) return;
     char* xh = Xbuf + buf * XBUF;
+    const int g = HFG_UPS_ROT ? (xq & 1) + ((xq >> 1) & 2) : 0;
+    f4 xr[8];
+    bool okr[4];
 #pragma unroll
-    for (int tt = 0; tt < 4; ++tt) {
+    for (int e = 0; e < 8; ++e) xr[e] = xv[e];
+#pragma unroll
+    for (int tt = 0; tt < 4; ++tt) okr[tt] = okt[tt];
+    if (HFG_UPS_ROT) {
+      const bool b0 = g & 1, b1 = g & 2;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        f4 y;
+#pragma unroll
+        for (int tt = 0; tt < 4; ++tt) y[tt] = b0 ? xr[e][(tt + 1) & 3] : xr[e][tt];
+#pragma unroll
+        for (int tt = 0; tt < 4; ++tt) xr[e][tt] = b1 ? y[(tt + 2) & 3] : y[tt];
+      }
+      bool oy[4];
+#pragma unroll
+      for (int tt = 0; tt < 4; ++tt) oy[tt] = b0 ? okr[(tt + 1) & 3] : okr[tt];
+#pragma unroll
+      for (int tt = 0; tt < 4; ++tt) okr[tt] = b1 ? oy[(tt + 2) & 3] : oy[tt];
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
       bf16x8 hv, lv;
 #pragma unroll
       for (int e = 0; e < 8; e += 2) {
         floatx2 a;
-        a[0] = okt[tt] ? fmaxf(xv[e][tt] * sx, xv[e][tt] * sx1) : 0.f;
-        a[1] = okt[tt] ? fmaxf(xv[e + 1][tt] * sx, xv[e + 1][tt] * sx1) : 0.f;
+        a[0] = okr[j] ? fmaxf(xr[e][j] * sx, xr[e][j] * sx1) : 0.f;
+        a[1] = okr[j] ? fmaxf(xr[e + 1][j] * sx, xr[e + 1][j] * sx1) : 0.f;
         bf16x2 hh, ll;
         split2<FMT>(a, hh, ll);
         hv[e] = hh[0];
@@ -175,7 +209,7 @@ ups_bf16x3(const UpsParams p) {
         lv[e] = ll[0];
         lv[e + 1] = ll[1];
       }
-      const int r = 4 * xq + tt;
+      const int r = 4 * xq + ((j + g) & 3);
       const int off = r * 32 + 16 * (hf ^ ((r >> 3) & 1));
       *reinterpret_cast<bf16x8*>(xh + off) = hv;
       *reinterpret_cast<bf16x8*>(xh + XPLANE + off) = lv;
