@@ -376,7 +376,10 @@ def test_resblock_stream_packing_and_windowing(pkg, preset, precision):
             assert Cc == Cst and KT == cfg.resblock_kernel_sizes[j]
             dils = cfg.resblock_dilation_sizes[j]
             assert n_conv == 2 * len(dils)
-            assert info["halo"] == sum((KT - 1) // 2 * d + (KT - 1) // 2 for d in dils)
+            # the first conv is exact on the whole window (margins staged from x): the halo
+            # is the radius of the convs after it
+            assert info["halo"] == sum((KT - 1) // 2 * d + (KT - 1) // 2 for d in dils) \
+                - (KT - 1) // 2 * dils[0]
             # W is rounded down to a multiple of 4 (16-B aligned block origins)
             nwin = next(n for n in (256, 512, 1024) if 0 <= n - info["W"] - 2 * info["halo"] < 4)
             assert info["W"] % 4 == 0
@@ -417,16 +420,30 @@ def test_resblock_stream_packing_and_windowing(pkg, preset, precision):
                     xx = xx + _conv_same(t, w2, b2, 1)
                 return xx
 
+            def resblock_window(xe, ve, r0):
+                """the kernel's window: the first conv reads r0 columns of x past either
+                edge (the LDS margins) and is kept on the window only; later convs see the
+                window alone (zero padding of the window itself emulates the arbitrary data
+                past its edges: any value gives the same centre)"""
+                (w1, b1), (w2, b2) = Ws[0], Ws[1]
+                t = _conv_same(_lrelu(xe) * ve, w1, b1, dils[0])[:, r0:r0 + nwin]
+                xx, valid = xe[:, r0:r0 + nwin], ve[r0:r0 + nwin]
+                xx = xx + _conv_same(_lrelu(t) * valid, w2, b2, 1)
+                for m in range(1, len(dils)):
+                    (w1, b1), (w2, b2) = Ws[2 * m], Ws[2 * m + 1]
+                    t = _lrelu(_conv_same(_lrelu(xx) * valid, w1, b1, dils[m])) * valid
+                    xx = xx + _conv_same(t, w2, b2, 1)
+                return xx
+
             direct = resblock(x[:, :ln], np.ones(ln))
             out = np.zeros((Cc, ln))
+            r0 = (KT - 1) // 2 * dils[0]
             for t0 in range(0, ln, info["W"]):
                 ws = t0 - info["halo"]
-                cols = ws + np.arange(nwin)
+                cols = ws - r0 + np.arange(nwin + 2 * r0)
                 valid = ((cols >= 0) & (cols < ln)).astype(np.float64)
                 xw = np.where(valid > 0, x[:, np.clip(cols, 0, L - 1)], 0.0)
-                # edges see arbitrary data past the window: emulate with zero padding of the
-                # window itself (any value gives the same centre)
-                yw = resblock(xw, valid)
+                yw = resblock_window(xw, valid, r0)
                 c0, c1 = info["halo"], info["halo"] + min(info["W"], ln - t0)
                 out[:, t0:t0 + (c1 - c0)] = yw[:, c0:c1]
             assert np.abs(out - direct).max() < 1e-9

@@ -71,7 +71,7 @@ __device__ __forceinline__ floatx4_ mfma16(const bf16x8& a, const bf16x8& b, con
 // HFG_SPLIT_MIX (f16): the residual a - f32(hi) as one v_fma_mix_f32 per value (hi read as
 // f16 straight from the packed pair) instead of a conversion back plus a subtraction
 #ifndef HFG_SPLIT_MIX
-#define HFG_SPLIT_MIX 0
+#define HFG_SPLIT_MIX 1
 #endif
 template <int FMT>
 __device__ __forceinline__ void split2(const floatx2_& a, bf16x2_& hi, bf16x2_& lo) {

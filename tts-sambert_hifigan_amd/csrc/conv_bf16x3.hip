@@ -504,7 +504,7 @@ conv1d_bf16x3(const ConvParams p) {
             if constexpr (AD == 2) a1[pl][i] = a2[pl][i];
           }
       }
-      lds_barrier();
+      if (!(kAblate && (p.dbg & 4))) lds_barrier();
     }
   } else if constexpr (KT_ > 0 && WM * WN >= 8) {
     // ---- 64x128-per-wave tile, compile-time taps: the chunk loop unrolled over one

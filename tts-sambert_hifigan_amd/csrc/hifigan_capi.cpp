@@ -441,6 +441,9 @@ int build_layers(hfg_handle* h) {
         rb.halo += (rb.kt - 1) / 2 * c.dil[j][m] + (rb.kt - 1) / 2;
         if ((rb.kt - 1) / 2 * c.dil[j][m] > hfg::rb_marg(C, waves_n)) ok = false;
       }
+      // the first conv of a launch reads its radius of x beyond the window (the LDS margin
+      // rows) and is exact on the whole window: the halo is the radius of the convs after it
+      rb.halo -= (rb.kt - 1) / 2 * c.dil[j][0];
       // a multiple of 4: block origins t0 = W * blockIdx stay 16-B aligned for the
       // LDS-staged float4 MRF epilogue (which column a block computes does not change
       // its arithmetic: bitwise the same result for any W)
@@ -461,6 +464,8 @@ int build_layers(hfg_handle* h) {
           int h0 = 0, h1 = 0;
           for (int q = 0; q < m; ++q) h0 += hd[q];
           for (int q = m; q < c.n_dil[j]; ++q) h1 += hd[q];
+          h0 -= (rb.kt - 1) / 2 * c.dil[j][0];  // each part's first conv: exact (margins)
+          h1 -= (rb.kt - 1) / 2 * c.dil[j][m];
           const int w0 = (nwin - 2 * h0) & ~3, w1 = (nwin - 2 * h1) & ~3;
           if (w0 < nwin / 4 || w1 < nwin / 4) continue;
           const double cost = ((double)m * nwin / w0 + (double)(c.n_dil[j] - m) * nwin / w1) /

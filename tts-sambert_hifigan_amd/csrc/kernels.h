@@ -64,7 +64,8 @@ struct ConvParams {
   int ew;
   int dbg;           // ablation flags (HFG_DEBUG_FLAGS, builds with -DHFG_ABLATE=1 only; wrong
                      // results when set), bf16x3 kernel: bit0 skip input restaging after the
-                     // first chunk, bit2 no per-chunk barrier, bit3 no epilogue
+                     // first chunk, bit2 no per-chunk barrier, bit3 no epilogue, bit7 every
+                     // group's input loads re-read group 0 (L2-warm)
 };
 
 // kernel ablation switches (timing experiments) exist only in -DHFG_ABLATE=1 builds

@@ -7,10 +7,12 @@
 //
 // A block owns a window of NWIN time columns [ws, ws + NWIN) of one utterance and
 // writes the centre [ws + halo, ws + halo + W), W = NWIN - 2*halo, where halo is the
-// ResBlock's receptive-field radius (sum over its convs of (k-1)/2 * dilation).  All
-// 2*n_dil convs run on the whole window; columns within a conv's radius of the window
-// edge become garbage and the garbage front moves inwards by exactly that radius, so
-// the centre is exact.  Columns outside [0, len) are re-zeroed after every conv — the
+// receptive-field radius of the launch's convs after the first (sum of (k-1)/2 * dilation).
+// All convs run on the whole window.  The first conv's operand also covers its radius on
+// either side (the LDS margin rows, staged from x), so its output is exact on the whole
+// window; from the second conv on, the columns within a conv's radius of the window edge
+// become garbage and the garbage front moves inwards by exactly that radius, so the
+// centre is exact.  Columns outside [0, len) are re-zeroed after every conv — the
 // reference's zero padding of each conv input.
 //
 // State: the residual stream x lives in registers (fp32, MFMA accumulator layout:
@@ -38,7 +40,19 @@
 #include "bf16x3_common.h"
 #include "kernels.h"
 
+// diagnostic build only (-DHFG_RB_TIMING=1, profiles/r04): wave 0 of every block stamps the
+// shader clock at the phase boundaries into g_rb_ts (one region per instance and launch half),
+// read back by hfg_debug_rb_ts (tests/tools/rb_phases.py)
+#ifndef HFG_RB_TIMING
+#define HFG_RB_TIMING 0
+#endif
+
 namespace hfg {
+
+#if HFG_RB_TIMING
+constexpr int kRbTsSlots = 24, kRbTsBlocks = 8192, kRbTsRegions = 20;
+__device__ uint64_t g_rb_ts[kRbTsRegions * kRbTsBlocks * kRbTsSlots];
+#endif
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 typedef float floatx2 __attribute__((ext_vector_type(2)));
@@ -55,8 +69,9 @@ resblock_bf16x3(const RbParams p) {
   constexpr int NWIN = 32 * WN * WAVES_N;  // window columns
   constexpr int STEPS = NG * KT;           // MFMA k-steps per conv
   static_assert(STEPS % 2 == 0, "two-deep A register ring needs an even step count");
-  // operand rows: the window plus MARG spare rows on each side, read (never written)
-  // by the taps of edge columns; their contents only reach garbage columns
+  // operand rows: the window plus MARG spare rows on each side, read by the taps of edge
+  // columns: the first conv's operand fills its radius of them from x (write_margins), later
+  // operands leave them stale (their contents only reach garbage columns)
   constexpr int MARG = rb_marg(C, WAVES_N);
   constexpr int ROWS = NWIN + 2 * MARG;
   constexpr int PS = ROWS * 16;            // bytes per plane: [row][8 bf16]
@@ -80,6 +95,23 @@ resblock_bf16x3(const RbParams p) {
   const int len_b = p.len ? min(p.len[b], p.L) : p.L;
   const int t0 = blockIdx.x * p.W;
   if (t0 >= len_b) return;  // whole block past this utterance's end (block-uniform)
+#if HFG_RB_TIMING
+  const int ts_region = ((KT == 3 ? 0 : KT == 7 ? 1 : 2) * 3 + (WAVES_M == 1 ? 0 : WAVES_M == 2 ? 1 : 2)) * 2 +
+                        (p.conv0 > 0 ? 1 : 0) + (WAVES_N == 2 && WAVES_M == 2 ? 18 : 0) - (WAVES_N == 2 && WAVES_M == 2 ? 2 : 0);
+  const int ts_blk = blockIdx.y * gridDim.x + blockIdx.x;
+  uint64_t* const ts = g_rb_ts + ((size_t)ts_region * kRbTsBlocks + (ts_blk < kRbTsBlocks ? ts_blk : 0)) * kRbTsSlots;
+  auto stamp = [&](int i) {
+    const uint64_t t = __builtin_amdgcn_s_memtime();
+    if (tid == 0) ts[i] = t;
+  };
+  {
+    const uint64_t r = __builtin_amdgcn_s_memrealtime();
+    if (tid == 0) ts[0] = r;
+  }
+  stamp(1);
+#else
+  auto stamp = [](int) {};
+#endif
   const int ws = t0 - p.halo;
   const int cbase = wave_n * 32 * WN;      // first window column of this wave
   const int row0 = wave_m * 32;
@@ -111,6 +143,7 @@ resblock_bf16x3(const RbParams p) {
   };
   load_a(0, Q0);
   load_a(1, Q0 + 1);
+  stamp(20);
 
   // ---- x and the MRF accumulator of utterance b through buffer descriptors ----
   // Element (row, column) sits at soffset = (row0 + row part of accumulator element r) * L * 4
@@ -144,6 +177,57 @@ resblock_bf16x3(const RbParams p) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) xcur[k][r] = (vk[k] && !xz) ? xcur[k][r] : 0.f;
   }
+  // ---- the first conv's margins: operand columns [-R0, 0) and [NWIN, NWIN + R0) of the
+  // window read from x (R0 = that conv's receptive-field radius <= MARG, host-checked), so the
+  // first conv is exact on the whole window and the launch's halo leaves out its radius.  One
+  // task = one column of one half-group: its 8 slot channels (write_operand's permutation) ----
+  constexpr int MG_T = (4 * MARG * NG + NT - 1) / NT;  // margin tasks per thread
+  const int R0 = (KT - 1) / 2 * p.dil[0];
+  const int n_mg = 4 * R0 * NG;
+  float mg[MG_T][8];
+  bool mg_ok[MG_T];
+  int mg_off[MG_T];  // byte offset of the task's 16-B row in the hi plane
+#pragma unroll
+  for (int q = 0; q < MG_T; ++q) {
+    const int t = tid + q * NT;
+    const int hh = t & 1, gq = (t >> 1) % NG, m = (t >> 1) / NG;
+    const int c = m < R0 ? m - R0 : NWIN + m - R0;  // window column
+    const int gc = ws + c;
+    const bool ok = t < n_mg && (unsigned)gc < (unsigned)len_b;
+    mg_ok[q] = ok;
+    mg_off[q] = gq * GS + hh * HPS + (c + MARG) * 16;
+    const unsigned vo = ok ? ((unsigned)(16 * gq + 4 * hh) * (unsigned)p.L + (unsigned)gc) * 4u : 0u;
+#pragma unroll
+    for (int e = 0; e < 8; ++e)
+      mg[q][e] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                               xrs, (int)vo, (int)(((e & 3) + 8 * (e >> 2)) * Lb), 0));
+  }
+#pragma unroll
+  for (int q = 0; q < MG_T; ++q)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) mg[q][e] = mg_ok[q] ? mg[q][e] : 0.f;
+  auto write_margins = [&](float sc) {
+#pragma unroll
+    for (int q = 0; q < MG_T; ++q) {
+      if (tid + q * NT < n_mg) {
+        bf16x8 h, l;
+#pragma unroll
+        for (int e = 0; e < 8; e += 2) {
+          floatx2 a;
+          a[0] = fmaxf(mg[q][e] * sc, mg[q][e] * (kLReluSlope * sc));
+          a[1] = fmaxf(mg[q][e + 1] * sc, mg[q][e + 1] * (kLReluSlope * sc));
+          bf16x2 hh, ll;
+          split2<FMT>(a, hh, ll);
+          h[e] = hh[0];
+          h[e + 1] = hh[1];
+          l[e] = ll[0];
+          l[e + 1] = ll[1];
+        }
+        *reinterpret_cast<bf16x8*>(lds + mg_off[q]) = h;
+        *reinterpret_cast<bf16x8*>(lds + mg_off[q] + PS) = l;
+      }
+    }
+  };
 
   // lane's byte address of window column (cbase + col) in its half-group's hi plane
   const int vb = half * HPS + (cbase + col + MARG) * 16;
@@ -194,8 +278,7 @@ resblock_bf16x3(const RbParams p) {
   // make the scale depend on earlier launches; garbage that overflows f16 stays in garbage
   // columns.  Each wave posts its max before the barrier that ends every read of the previous
   // operand, and all read the NW maxima after it.
-  auto wave_amax = [&](const floatx16 (&v)[WN], int radius) {
-    float m = 0.f;
+  auto wave_amax = [&](const floatx16 (&v)[WN], int radius, float m = 0.f) {
 #pragma unroll
     for (int k = 0; k < WN; ++k) {
       const int c = cbase + 32 * k + col;
@@ -216,12 +299,24 @@ resblock_bf16x3(const RbParams p) {
   int ex = 0;
   int radius = 0;  // f16x3: receptive-field radius of the convs run so far
   if constexpr (FMT == kFmtF16) {
-    wave_amax(xcur, 0);
+#if HFG_RB_TIMING
+    wait_vm<0>();
+    stamp(21);
+#endif
+    float mm = 0.f;  // the margin columns are part of the first operand
+#pragma unroll
+    for (int q = 0; q < MG_T; ++q)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) mm = fmaxf(mm, fabsf(mg[q][e]));
+    wave_amax(xcur, 0, mm);
     lds_barrier();
     ex = block_exp();
+    stamp(22);
   }
   write_operand(xcur, exp2i(ex));
+  write_margins(exp2i(ex));
   lds_barrier();
+  stamp(2);
 
   // conv cv over the whole window: acc = bias + W_cv * operand (one LDS barrier at the
   // end: every wave has read the operand, which the caller then overwrites in place)
@@ -309,14 +404,17 @@ resblock_bf16x3(const RbParams p) {
   } else {
     for (int cv = 0; cv < n_conv; cv += 2) {
       run_conv(cv);
+      stamp(3 + 2 * cv);
       finalize(cv);
-      radius += (KT - 1) / 2 * p.dil[cv];
+      if (cv > 0) radius += (KT - 1) / 2 * p.dil[cv];  // conv 0: exact (margins from x)
       wave_amax(acc, radius);
       lds_barrier();  // every wave is done reading the operand; the maxima are posted
       ex = block_exp();
       write_operand(acc, exp2i(ex));
       lds_barrier();
+      stamp(4 + 2 * cv);
       run_conv(cv + 1);
+      stamp(5 + 2 * cv);
       finalize(cv + 1);
       radius += (KT - 1) / 2;  // conv2: dilation 1
 #pragma unroll
@@ -330,6 +428,7 @@ resblock_bf16x3(const RbParams p) {
         write_operand(xcur, exp2i(ex));
         lds_barrier();
       }
+      stamp(6 + 2 * cv);
     }
   }
 
@@ -361,6 +460,10 @@ resblock_bf16x3(const RbParams p) {
       for (int r = 0; r < 16; ++r)
         mv[k][r] = __builtin_bit_cast(
             float, __builtin_amdgcn_raw_buffer_load_b32(mrs, (int)vo[k], (int)srow(r), 0));
+#if HFG_RB_TIMING
+    wait_vm<0>();
+    stamp(23);
+#endif
 #pragma unroll
     for (int k = 0; k < WN; ++k)
 #pragma unroll
@@ -393,6 +496,13 @@ resblock_bf16x3(const RbParams p) {
       }
     }
   }
+  stamp(3 + 2 * n_conv);
+#if HFG_RB_TIMING
+  {
+    const uint64_t r = __builtin_amdgcn_s_memrealtime();
+    if (tid == 0) ts[4 + 2 * n_conv] = r;
+  }
+#endif
   if (p.amax_out) {  // f16x3 consumers of the stage output (block-uniform branch)
     float m = 0.f;
 #pragma unroll
@@ -478,3 +588,15 @@ hipError_t launch_resblock_bf16x3(int C, int waves_n, int kt, int fmt, int np, c
 }
 
 }  // namespace hfg
+
+#if HFG_RB_TIMING
+extern "C" int hfg_debug_rb_ts(void* dst, size_t bytes) {
+  if (bytes > sizeof(hfg::g_rb_ts)) bytes = sizeof(hfg::g_rb_ts);
+  return (int)hipMemcpyFromSymbol(dst, HIP_SYMBOL(hfg::g_rb_ts), bytes, 0, hipMemcpyDeviceToHost);
+}
+extern "C" int hfg_debug_rb_ts_clear() {
+  static uint64_t* z = nullptr;
+  if (!z) z = (uint64_t*)calloc(1, sizeof(hfg::g_rb_ts));
+  return (int)hipMemcpyToSymbol(HIP_SYMBOL(hfg::g_rb_ts), z, sizeof(hfg::g_rb_ts), 0, hipMemcpyHostToDevice);
+}
+#endif

@@ -166,7 +166,7 @@ ups_bf16x3(const UpsParams p) {
   // rotated in registers by g first (2 selects per value); the layout and the readers are
   // unchanged.
 #ifndef HFG_UPS_ROT
-#define HFG_UPS_ROT 1
+#define HFG_UPS_ROT 0
 #endif
   auto store_x = [&](int buf) {
     if (!has_task) return;
