@@ -62,7 +62,7 @@ PEAK_BF16_TFLOPS = 2500.0  # MI355X_MICROARCH.md: BF16 MFMA dense (no sparsity)
 
 # position of the NP (MFMA products per multiply-add) and FMT (split format) template
 # arguments of the split-precision kernels, as hfg_profile_summary / rocprofv3 print them
-_SPLIT_ARGS = {"conv1d_bf16x3": (8, 10), "ups_bf16x3": (4, 5), "resblock_bf16x3": (3, 4),
+_SPLIT_ARGS = {"conv1d_bf16x3": (8, 10), "ups_bf16x3": (4, 5), "resblock_bf16x3": (4, 5),
                "mrf_thin_mfma": (1, 2)}
 
 

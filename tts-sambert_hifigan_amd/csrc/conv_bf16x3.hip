@@ -47,7 +47,19 @@
 #define HFG_AREG_NVST 6
 #endif
 
+// diagnostic build only (-DHFG_CONV_TIMING=1, profiles/r04): wave 0 of every tile-5 block
+// stamps the shader clock (start, prologue end, loop end, epilogue end) and sums its
+// barrier waits into g_cv_ts (one region per KT), read back by hfg_debug_cv_ts
+#ifndef HFG_CONV_TIMING
+#define HFG_CONV_TIMING 0
+#endif
+
 namespace hfg {
+
+#if HFG_CONV_TIMING
+constexpr int kCvTsSlots = 16, kCvTsBlocks = 8192, kCvTsRegions = 12;
+__device__ uint64_t g_cv_ts[kCvTsRegions * kCvTsBlocks * kCvTsSlots];
+#endif
 
 namespace {
 typedef float floatx2 __attribute__((ext_vector_type(2)));
@@ -373,6 +385,21 @@ conv1d_bf16x3(const ConvParams p) {
     __builtin_amdgcn_sched_barrier(0);
   };
 
+#if HFG_CONV_TIMING
+  uint64_t* const cts = g_cv_ts + ((size_t)((KT_ == 3 ? 0 : KT_ == 7 ? 1 : KT_ == 11 ? 2 : 3) * 3 +
+                                           (p.res ? ((p.mrf && (p.mrf_mode & 1)) ? 2 : 1) : 0)) * kCvTsBlocks +
+                                   ((blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x) % kCvTsBlocks) *
+                                      kCvTsSlots;
+  auto cstamp = [&](int i) {
+    const uint64_t t = __builtin_amdgcn_s_memtime();
+    if (AREG && tid == 0) cts[i] = t;
+  };
+  uint64_t bar_wait = 0;
+  if (AREG && tid == 0) cts[0] = __builtin_amdgcn_s_memrealtime();
+  cstamp(1);
+#else
+  auto cstamp = [](int) {};
+#endif
   // ---- prologue: weight slabs of chunks 0..WD-2, input window of channel group 0 ----
   load_x(0);
   if constexpr (!AREG) {
@@ -383,6 +410,7 @@ conv1d_bf16x3(const ConvParams p) {
   store_x(Xbuf0);
   wait_vm<0>();
   lds_barrier();
+  cstamp(2);
 
   if constexpr (AREG) {
     // ---- A fragments from global into registers, AD taps ahead; one barrier per
@@ -434,7 +462,9 @@ conv1d_bf16x3(const ConvParams p) {
       const int off = half * HPS_AREG + (wave_n * 32 * WN + col) * 8 + (k % WN) * 32 * 8 +
                       (tap + k / WN) * p.dil * 8;
       bh[k & 1] = *reinterpret_cast<const bf16x8*>(Xh + off);
-      bl[k & 1] = *reinterpret_cast<const bf16x8*>(Xh + xplane + off);
+      // ablation bit 12: no lo-plane reads (the hi fragment stands in; half the LDS reads)
+      bl[k & 1] = (kAblate && (p.dbg & 4096)) ? bh[k & 1]
+                                              : *reinterpret_cast<const bf16x8*>(Xh + xplane + off);
     };
     static_assert(WN % 2 == 0, "B ring parity across taps");
     auto tap_regs = [&](const ASet& a, const __bf16* Xh, int tap, bool pre_in, bool pre_out) {
@@ -504,8 +534,18 @@ conv1d_bf16x3(const ConvParams p) {
             if constexpr (AD == 2) a1[pl][i] = a2[pl][i];
           }
       }
+#if HFG_CONV_TIMING
+      const uint64_t tb0 = __builtin_amdgcn_s_memtime();
+#endif
       if (!(kAblate && (p.dbg & 4))) lds_barrier();
+#if HFG_CONV_TIMING
+      bar_wait += __builtin_amdgcn_s_memtime() - tb0;
+#endif
     }
+#if HFG_CONV_TIMING
+    if (tid == 0) cts[5] = bar_wait;
+#endif
+    cstamp(3);
   } else if constexpr (KT_ > 0 && WM * WN >= 8) {
     // ---- 64x128-per-wave tile, compile-time taps: the chunk loop unrolled over one
     // channel group, so the chunks that stage the next input window are their own
@@ -745,6 +785,7 @@ conv1d_bf16x3(const ConvParams p) {
       // outstanding; they count in vmcnt, not lgkmcnt)
       wait_vm<0>();
       lds_barrier();
+      cstamp(7);
       float* stage = reinterpret_cast<float*>(lds16) + wave * 32 * (32 * WN + 8);
       conv_epilogue_lds<WM, WN>(p, acc, b, mt * MT + wave_m * 32 * WM, n0 + wave_n * 32 * WN,
                                 N_b, half, col, stage, lane, sc);
@@ -753,6 +794,10 @@ conv1d_bf16x3(const ConvParams p) {
                             half, col, sc);
     }
   }
+  cstamp(4);
+#if HFG_CONV_TIMING
+  if (AREG && tid == 0) cts[6] = __builtin_amdgcn_s_memrealtime();
+#endif
 }
 
 namespace {
@@ -845,3 +890,15 @@ hipError_t launch_conv_bf16x3(int tile, int kt, bool ups, int fmt, int np, const
 }
 
 }  // namespace hfg
+
+#if HFG_CONV_TIMING
+extern "C" int hfg_debug_cv_ts(void* dst, size_t bytes) {
+  if (bytes > sizeof(hfg::g_cv_ts)) bytes = sizeof(hfg::g_cv_ts);
+  return (int)hipMemcpyFromSymbol(dst, HIP_SYMBOL(hfg::g_cv_ts), bytes, 0, hipMemcpyDeviceToHost);
+}
+extern "C" int hfg_debug_cv_ts_clear() {
+  static uint64_t* z = nullptr;
+  if (!z) z = (uint64_t*)calloc(1, sizeof(hfg::g_cv_ts));
+  return (int)hipMemcpyToSymbol(HIP_SYMBOL(hfg::g_cv_ts), z, sizeof(hfg::g_cv_ts), 0, hipMemcpyHostToDevice);
+}
+#endif

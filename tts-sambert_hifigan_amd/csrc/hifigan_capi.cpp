@@ -116,7 +116,7 @@ struct ProfRec {
 struct RbFused {
   std::vector<int> convs;     // layer indices in execution order conv1_0, conv2_0, conv1_1, ...
   bool fused = false;         // this ResBlock runs as one resblock_bf16x3 launch
-  int kt = 0, halo = 0, W = 0, waves_n = 0;
+  int kt = 0, halo = 0, W = 0, nwin = 0, wm = 1;  // window columns, row tiles per wave
   // split into two launches (convs [0, split) then [split, n)): each part's window pays
   // only its own receptive-field halo; the first writes x to scratch (0: one launch)
   int split = 0;
@@ -430,16 +430,16 @@ int build_layers(hfg_handle* h) {
       rb.kt = c.res_kernels[j];
       // C = 64, k = 3: a 256-column window (5 % more halo recompute than 512) whose small
       // LDS footprint lets two blocks share a CU and overlap their operand rewrites
-      const int waves_n = C == 128 ? 2 : C == 64 ? (rb.kt == 3 ? 2 : 4) : 4;
-      const int nwin = hfg::kRbColsPerWave * waves_n;
-      rb.waves_n = waves_n;
-      bool ok = rb.kt % 2 == 1 && hfg::rb_supported(C, rb.kt, waves_n) &&
+      const int nwin = C == 128 ? 256 : C == 64 ? (rb.kt == 3 ? 256 : 512) : 512;
+      rb.nwin = nwin;
+      rb.wm = 1;
+      bool ok = rb.kt % 2 == 1 && hfg::rb_supported(C, rb.kt, nwin, rb.wm) &&
                 2 * c.n_dil[j] <= hfg::kRbMaxConv;
       for (int m = 0; m < c.n_dil[j]; ++m, ++idx) {
         rb.convs.push_back(st.conv1[idx]);
         rb.convs.push_back(st.conv2[idx]);
         rb.halo += (rb.kt - 1) / 2 * c.dil[j][m] + (rb.kt - 1) / 2;
-        if ((rb.kt - 1) / 2 * c.dil[j][m] > hfg::rb_marg(C, waves_n)) ok = false;
+        if ((rb.kt - 1) / 2 * c.dil[j][m] > hfg::rb_marg(C, nwin)) ok = false;
       }
       // the first conv of a launch reads its radius of x beyond the window (the LDS margin
       // rows) and is exact on the whole window: the halo is the radius of the convs after it
@@ -1151,7 +1151,8 @@ int run_resblock(hfg_handle* h, Launcher& ln, const RbFused& rb, const float* x,
     const char* name = nullptr;
     ln.begin(flop, bytes);
     hipError_t e =
-        hfg::launch_resblock_bf16x3(C, rb.waves_n, rb.kt, h->fmt, h->np, p, (int)B, ln.stream, &name);
+        hfg::launch_resblock_bf16x3(C, rb.nwin, rb.wm, rb.kt, h->fmt, h->np, p, (int)B, ln.stream,
+                                    &name);
     ln.end(name);
     if (e != hipSuccess)
       return fail(HFG_EIO, "launch resblock %s: %s", L0.mod.c_str(), hipGetErrorString(e));

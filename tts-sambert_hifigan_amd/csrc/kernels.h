@@ -218,15 +218,15 @@ hipError_t launch_ups_bf16x3(int cfg, int fmt, int np, const UpsParams& p, hipSt
                              const char** name);
 
 // ---- whole ResBlock per launch (resblock_bf16x3.hip) ----
-// All 2*n_dil convs of one ResBlock of a C in {32, 64} stage on a window of
-// kRbColsPerWave * waves_n columns; x in registers, the conv operand in LDS.
-constexpr int kRbColsPerWave = 128;
+// All 2*n_dil convs of one ResBlock of a C in {32, 64, 128} stage on a window of nwin
+// columns (256 or 512); x in registers, the conv operand in LDS.  Each wave owns wm row
+// tiles (32 or 64 rows) x 4/wm column tiles.
 constexpr int kRbMaxConv = 16;
-// spare operand rows per side (every conv's (k-1)/2*dil must fit): 48 for C <= 64, 28 for
-// C = 128 (its 256-column window then just fits the 160 KB LDS), 16 for the narrow C = 64
-// window (256 columns: 74 KB, two blocks per CU, used for k = 3)
-constexpr int rb_marg(int C, int waves_n) {
-  return C >= 128 ? 28 : (C == 64 && waves_n == 2) ? 16 : 48;
+// spare operand rows per side (every conv's (k-1)/2*dil must fit): 48 for the 512-column
+// windows, 28 for C = 128 (its 256-column window then just fits the 160 KB LDS), 16 for the
+// narrow C = 64 window (256 columns: 74 KB, two blocks per CU, used for k = 3)
+constexpr int rb_marg(int C, int nwin) {
+  return C >= 128 ? 28 : (C == 64 && nwin == 256) ? 16 : 48;
 }
 struct RbParams {
   const float* x;        // stage input [B][C][L]
@@ -255,10 +255,11 @@ struct RbParams {
 inline bool fast_div_ok(float d) {
   return d == 1.f || d == 2.f || d == 3.f || d == 4.f || d == 5.f || d == 7.f || d == 8.f;
 }
-bool rb_supported(int C, int kt, int waves_n);
-size_t rb_lds_bytes(int C, int waves_n, int n_conv);
-hipError_t launch_resblock_bf16x3(int C, int waves_n, int kt, int fmt, int np, const RbParams& p,
-                                  int batch, hipStream_t stream, const char** name);
+bool rb_supported(int C, int kt, int nwin, int wm);
+size_t rb_lds_bytes(int C, int nwin, int n_conv);
+hipError_t launch_resblock_bf16x3(int C, int nwin, int wm, int kt, int fmt, int np,
+                                  const RbParams& p, int batch, hipStream_t stream,
+                                  const char** name);
 
 // ---- whole MRF per launch for thin stages, C <= 16 (mrf_thin.hip) ----
 // All ResBlocks of one MRF on a time window in LDS, packed-fp32 VALU dot products (exact

@@ -58,21 +58,22 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 typedef float floatx2 __attribute__((ext_vector_type(2)));
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 
-template <int KT, int WAVES_M, int WAVES_N, int NP, int FMT>
+template <int KT, int WAVES_M, int WAVES_N, int WM, int NP, int FMT>
 __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N, 2)  // 2 waves/SIMD: <= 256 VGPRs
 resblock_bf16x3(const RbParams p) {
   constexpr int NW = WAVES_M * WAVES_N;
   constexpr int NT = 64 * NW;
-  constexpr int C = 32 * WAVES_M;
+  static_assert(WM == 1 || WM == 2, "32 or 64 rows per wave");
+  constexpr int C = 32 * WM * WAVES_M;
   constexpr int NG = C / 16;               // 16-channel groups
-  constexpr int WN = 4;                    // 32-column MFMA tiles per wave
+  constexpr int WN = 4 / WM;               // 32-column MFMA tiles per wave (WM row tiles)
   constexpr int NWIN = 32 * WN * WAVES_N;  // window columns
   constexpr int STEPS = NG * KT;           // MFMA k-steps per conv
   static_assert(STEPS % 2 == 0, "two-deep A register ring needs an even step count");
   // operand rows: the window plus MARG spare rows on each side, read by the taps of edge
   // columns: the first conv's operand fills its radius of them from x (write_margins), later
   // operands leave them stale (their contents only reach garbage columns)
-  constexpr int MARG = rb_marg(C, WAVES_N);
+  constexpr int MARG = rb_marg(C, NWIN);
   constexpr int ROWS = NWIN + 2 * MARG;
   constexpr int PS = ROWS * 16;            // bytes per plane: [row][8 bf16]
   constexpr int HPS = 2 * PS;              // half-group (slots 0-7 | 8-15): hi, lo planes
@@ -96,8 +97,9 @@ resblock_bf16x3(const RbParams p) {
   const int t0 = blockIdx.x * p.W;
   if (t0 >= len_b) return;  // whole block past this utterance's end (block-uniform)
 #if HFG_RB_TIMING
-  const int ts_region = ((KT == 3 ? 0 : KT == 7 ? 1 : 2) * 3 + (WAVES_M == 1 ? 0 : WAVES_M == 2 ? 1 : 2)) * 2 +
-                        (p.conv0 > 0 ? 1 : 0) + (WAVES_N == 2 && WAVES_M == 2 ? 18 : 0) - (WAVES_N == 2 && WAVES_M == 2 ? 2 : 0);
+  const int ts_region = NWIN == 256 && C == 64 ? 18 + (p.conv0 > 0 ? 1 : 0)
+                        : ((KT == 3 ? 0 : KT == 7 ? 1 : 2) * 3 + (C == 32 ? 0 : C == 64 ? 1 : 2)) * 2 +
+                              (p.conv0 > 0 ? 1 : 0);
   const int ts_blk = blockIdx.y * gridDim.x + blockIdx.x;
   uint64_t* const ts = g_rb_ts + ((size_t)ts_region * kRbTsBlocks + (ts_blk < kRbTsBlocks ? ts_blk : 0)) * kRbTsSlots;
   auto stamp = [&](int i) {
@@ -114,7 +116,7 @@ resblock_bf16x3(const RbParams p) {
 #endif
   const int ws = t0 - p.halo;
   const int cbase = wave_n * 32 * WN;      // first window column of this wave
-  const int row0 = wave_m * 32;
+  const int row0 = wave_m * 32 * WM;     // first row of this wave (WM row tiles of 32)
   const int n_conv = p.n_conv;
   // A stream: the whole ResBlock's convs (p.n_conv_stream per wave row-block); this launch
   // runs convs p.conv0 .. p.conv0 + n_conv - 1 of it (a ResBlock split into two launches)
@@ -132,14 +134,18 @@ resblock_bf16x3(const RbParams p) {
   // ---- A stream (buffer loads: SGPR descriptor + scalar step offset, no address VALU) ----
   const __amdgpu_buffer_rsrc_t wrs =
       __builtin_amdgcn_make_buffer_rsrc((void*)p.w, 0, p.w_bytes, 0x00020000);
-  const int a_base = wave_m * QT * ASTEP;
+  const int a_base = wave_m * WM * QT * ASTEP;  // row tile i: + i * QT * ASTEP
   const int a_lane = lane * 16;
-  bf16x8 ra_h[2], ra_l[2];
+  bf16x8 ra_h[2][WM], ra_l[2][WM];
   auto load_a = [&](int slot, int q) {
     const int so = a_base + min(q, QT - 1) * ASTEP;
-    ra_h[slot] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(wrs, a_lane, so, 0));
-    ra_l[slot] =
-        __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(wrs, a_lane + 1024, so, 0));
+#pragma unroll
+    for (int i = 0; i < WM; ++i) {
+      ra_h[slot][i] = __builtin_bit_cast(
+          bf16x8, __builtin_amdgcn_raw_buffer_load_b128(wrs, a_lane, so + i * QT * ASTEP, 0));
+      ra_l[slot][i] = __builtin_bit_cast(
+          bf16x8, __builtin_amdgcn_raw_buffer_load_b128(wrs, a_lane + 1024, so + i * QT * ASTEP, 0));
+    }
   };
   load_a(0, Q0);
   load_a(1, Q0 + 1);
@@ -153,29 +159,33 @@ resblock_bf16x3(const RbParams p) {
   // 4-GiB item would lose its last float), so every offset and its dword end fit 32 bits;
   // the range is never relied on otherwise (masked lanes read offset 0).
   const unsigned Lb = (unsigned)p.L * 4u;
-  auto srow = [&](int r) { return (unsigned)(row0 + (r & 3) + 8 * (r >> 2)) * Lb; };
+  auto srow = [&](int i, int r) { return (unsigned)(row0 + 32 * i + (r & 3) + 8 * (r >> 2)) * Lb; };
   const unsigned lrow = 4u * (unsigned)half * (unsigned)p.L;
   const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(p.x + (int64_t)b * p.bs), 0, (int)0xFFFFFFFFu, 0x00020000);
 
   // ---- residual stream x: window -> registers (zero outside [0, len)) ----
-  floatx16 xcur[WN];
+  floatx16 xcur[WM][WN];
   {
 #pragma unroll
     for (int k = 0; k < WN; ++k) {
       const unsigned vo = vk[k] ? (lrow + (unsigned)(ws + cbase + 32 * k + col)) * 4u : 0u;
 #pragma unroll
-      for (int r = 0; r < 16; ++r)
-        xcur[k][r] = __builtin_bit_cast(
-            float, __builtin_amdgcn_raw_buffer_load_b32(xrs, (int)vo, (int)srow(r), 0));
+      for (int i = 0; i < WM; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          xcur[i][k][r] = __builtin_bit_cast(
+              float, __builtin_amdgcn_raw_buffer_load_b32(xrs, (int)vo, (int)srow(i, r), 0));
     }
     // ablation bit 5 zeroes x after the loads (a select on a uniform flag inside the load
     // expression made the compiler branch per element)
     const bool xz = kAblate && (dbg & 32);
 #pragma unroll
-    for (int k = 0; k < WN; ++k)
+    for (int i = 0; i < WM; ++i)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) xcur[k][r] = (vk[k] && !xz) ? xcur[k][r] : 0.f;
+      for (int k = 0; k < WN; ++k)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) xcur[i][k][r] = (vk[k] && !xz) ? xcur[i][k][r] : 0.f;
   }
   // ---- the first conv's margins: operand columns [-R0, 0) and [NWIN, NWIN + R0) of the
   // window read from x (R0 = that conv's receptive-field radius <= MARG, host-checked), so the
@@ -241,33 +251,35 @@ resblock_bf16x3(const RbParams p) {
   // The 8 accumulator rows a lane holds per 16-channel group are exactly the 8 slots
   // (one 16-B row of its half-group) it reads as a B fragment.
   // f16x3: the operand is scaled by sc = 2^e (block_exp) inside the same two factors
-  auto write_operand = [&](const floatx16 (&v)[WN], float sc) {
+  auto write_operand = [&](const floatx16 (&v)[WM][WN], float sc) {
     if (kAblate && (dbg & 64)) return;
 #pragma unroll
     for (int k = 0; k < WN; ++k) {
       const floatx2 f1k = vk[k] ? sc : 0.0f, f2k = vk[k] ? kLReluSlope * sc : 0.0f;
 #pragma unroll
-      for (int gg = 0; gg < 2; ++gg) {
-        bf16x8 h, l;
+      for (int i = 0; i < WM; ++i)
 #pragma unroll
-        for (int e = 0; e < 8; e += 2) {
-          floatx2 vv, a;
-          vv[0] = v[k][gg * 8 + e];
-          vv[1] = v[k][gg * 8 + e + 1];
-          const floatx2 p1 = vv * f1k, p2 = vv * f2k;  // v_pk_mul_f32
-          a[0] = fmaxf(p1[0], p2[0]);
-          a[1] = fmaxf(p1[1], p2[1]);
-          bf16x2 hh, ll;
-          split2<FMT>(a, hh, ll);
-          h[e] = hh[0];
-          h[e + 1] = hh[1];
-          l[e] = ll[0];
-          l[e + 1] = ll[1];
+        for (int gg = 0; gg < 2; ++gg) {
+          bf16x8 h, l;
+#pragma unroll
+          for (int e = 0; e < 8; e += 2) {
+            floatx2 vv, a;
+            vv[0] = v[i][k][gg * 8 + e];
+            vv[1] = v[i][k][gg * 8 + e + 1];
+            const floatx2 p1 = vv * f1k, p2 = vv * f2k;  // v_pk_mul_f32
+            a[0] = fmaxf(p1[0], p2[0]);
+            a[1] = fmaxf(p1[1], p2[1]);
+            bf16x2 hh, ll;
+            split2<FMT>(a, hh, ll);
+            h[e] = hh[0];
+            h[e + 1] = hh[1];
+            l[e] = ll[0];
+            l[e + 1] = ll[1];
+          }
+          char* dst = lds + (row0 / 16 + 2 * i + gg) * GS + vb + k * 512;
+          *reinterpret_cast<bf16x8*>(dst) = h;
+          *reinterpret_cast<bf16x8*>(dst + PS) = l;
         }
-        char* dst = lds + (wave_m * 2 + gg) * GS + vb + k * 512;
-        *reinterpret_cast<bf16x8*>(dst) = h;
-        *reinterpret_cast<bf16x8*>(dst + PS) = l;
-      }
     }
   };
   // f16x3: the block's largest |value| over the window's exact columns sets the power-of-two
@@ -278,13 +290,15 @@ resblock_bf16x3(const RbParams p) {
   // make the scale depend on earlier launches; garbage that overflows f16 stays in garbage
   // columns.  Each wave posts its max before the barrier that ends every read of the previous
   // operand, and all read the NW maxima after it.
-  auto wave_amax = [&](const floatx16 (&v)[WN], int radius, float m = 0.f) {
+  auto wave_amax = [&](const floatx16 (&v)[WM][WN], int radius, float m = 0.f) {
 #pragma unroll
     for (int k = 0; k < WN; ++k) {
       const int c = cbase + 32 * k + col;
-      float mk = 0.f;  // v_max3 over the column's 16 rows, one select per column
+      float mk = 0.f;  // v_max3 over the column's 16 x WM rows, one select per column
 #pragma unroll
-      for (int r = 0; r < 16; ++r) mk = fmaxf(mk, fabsf(v[k][r]));
+      for (int i = 0; i < WM; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) mk = fmaxf(mk, fabsf(v[i][k][r]));
       m = (vk[k] && c >= radius && c < NWIN - radius) ? fmaxf(m, mk) : m;
     }
     m = wave_max(m);
@@ -320,17 +334,19 @@ resblock_bf16x3(const RbParams p) {
 
   // conv cv over the whole window: acc = bias + W_cv * operand (one LDS barrier at the
   // end: every wave has read the operand, which the caller then overwrites in place)
-  floatx16 acc[WN];
+  floatx16 acc[WM][WN];
   auto run_conv = [&](int cv) {
     const int d = p.dil[cv];
     const int pad = (KT - 1) / 2 * d;
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      // f16x3: the bias joins after the unscale (finalize)
-      const float bv = FMT == kFmtF16 ? 0.f : bias_s[cv * C + row0 + rrow(r)];
+    for (int i = 0; i < WM; ++i)
 #pragma unroll
-      for (int k = 0; k < WN; ++k) acc[k][r] = bv;
-    }
+      for (int r = 0; r < 16; ++r) {
+        // f16x3: the bias joins after the unscale (finalize)
+        const float bv = FMT == kFmtF16 ? 0.f : bias_s[cv * C + row0 + 32 * i + rrow(r)];
+#pragma unroll
+        for (int k = 0; k < WN; ++k) acc[i][k][r] = bv;
+      }
     bf16x8 bh[2][WN], bl[2][WN];
     // step s = (group g, tap j): rows shifted by j*d - pad, one VALU add per step,
     // tiles / planes by immediate offsets
@@ -340,7 +356,9 @@ resblock_bf16x3(const RbParams p) {
 #pragma unroll
       for (int k = 0; k < WN; ++k) {
         bh[buf][k] = *reinterpret_cast<const bf16x8*>(src + k * 512);
-        bl[buf][k] = *reinterpret_cast<const bf16x8*>(src + k * 512 + PS);
+        // ablation bit 11: no lo-plane reads (the hi fragment stands in; half the LDS reads)
+        bl[buf][k] = (kAblate && (dbg & 2048)) ? bh[buf][k]
+                                               : *reinterpret_cast<const bf16x8*>(src + k * 512 + PS);
       }
     };
     const int qb = Q0 + cv * STEPS;
@@ -352,12 +370,14 @@ resblock_bf16x3(const RbParams p) {
       const int cur = s & 1;
       if (s + 1 < STEPS) load_b(cur ^ 1, s + 1);
 #pragma unroll
-      for (int k = 0; k < WN; ++k) {
-        if constexpr (NP == 3)  // the weights' lo plane (zero for bf16-valued weights: NP 2)
-          acc[k] = mfma32<FMT>(ra_l[cur], bh[cur][k], acc[k]);
-        acc[k] = mfma32<FMT>(ra_h[cur], bl[cur][k], acc[k]);
-        acc[k] = mfma32<FMT>(ra_h[cur], bh[cur][k], acc[k]);
-      }
+      for (int k = 0; k < WN; ++k)
+#pragma unroll
+        for (int i = 0; i < WM; ++i) {
+          if constexpr (NP == 3)  // the weights' lo plane (zero for bf16-valued weights: NP 2)
+            acc[i][k] = mfma32<FMT>(ra_l[cur][i], bh[cur][k], acc[i][k]);
+          acc[i][k] = mfma32<FMT>(ra_h[cur][i], bl[cur][k], acc[i][k]);
+          acc[i][k] = mfma32<FMT>(ra_h[cur][i], bh[cur][k], acc[i][k]);
+        }
       load_a(cur, qb + s + 2);
       if (s + 1 < STEPS) {
 #pragma unroll
@@ -367,8 +387,8 @@ resblock_bf16x3(const RbParams p) {
         }
       }
       __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);    // 2 MFMA
-      __builtin_amdgcn_sched_group_barrier(0x020, 2, 0);    // A loads
-      __builtin_amdgcn_sched_group_barrier(0x008, NP * WN, 0);  // rest of the MFMAs
+      __builtin_amdgcn_sched_group_barrier(0x020, 2 * WM, 0);  // A loads
+      __builtin_amdgcn_sched_group_barrier(0x008, NP * WM * WN, 0);  // rest of the MFMAs
       __builtin_amdgcn_sched_barrier(0);
     }
   };
@@ -376,11 +396,13 @@ resblock_bf16x3(const RbParams p) {
   auto finalize = [&](int cv) {
     const float inv = exp2i(-(ex + p.ew[cv]));
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const float bv = bias_s[cv * C + row0 + rrow(r)];
+    for (int i = 0; i < WM; ++i)
 #pragma unroll
-      for (int k = 0; k < WN; ++k) acc[k][r] = __builtin_fmaf(acc[k][r], inv, bv);
-    }
+      for (int r = 0; r < 16; ++r) {
+        const float bv = bias_s[cv * C + row0 + 32 * i + rrow(r)];
+#pragma unroll
+        for (int k = 0; k < WN; ++k) acc[i][k][r] = __builtin_fmaf(acc[i][k][r], inv, bv);
+      }
   };
 
   // dilation pairs: xt = lrelu(conv1(lrelu(x)) + b1); x = x + (conv2(xt) + b2)
@@ -393,9 +415,11 @@ resblock_bf16x3(const RbParams p) {
       run_conv(cv + 1);
       lds_barrier();
 #pragma unroll
-      for (int k = 0; k < WN; ++k)
+      for (int i = 0; i < WM; ++i)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) xcur[k][r] = xcur[k][r] + acc[k][r];
+        for (int k = 0; k < WN; ++k)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) xcur[i][k][r] = xcur[i][k][r] + acc[i][k][r];
       if (cv + 2 < n_conv) {
         write_operand(xcur, 1.0f);
         lds_barrier();
@@ -418,9 +442,11 @@ resblock_bf16x3(const RbParams p) {
       finalize(cv + 1);
       radius += (KT - 1) / 2;  // conv2: dilation 1
 #pragma unroll
-      for (int k = 0; k < WN; ++k)
+      for (int i = 0; i < WM; ++i)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) xcur[k][r] = xcur[k][r] + acc[k][r];
+        for (int k = 0; k < WN; ++k)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) xcur[i][k][r] = xcur[i][k][r] + acc[i][k][r];
       if (cv + 2 < n_conv) {
         wave_amax(xcur, radius);
         lds_barrier();
@@ -434,7 +460,7 @@ resblock_bf16x3(const RbParams p) {
 
   // ---- MRF: (mrf + x) [/ n_res] on the window centre ----
   if (kAblate && (dbg & 16)) {  // ablation: no MRF epilogue
-    if (xcur[0][0] == 1.2345e-30f) p.mrf[0] = xcur[WN - 1][15];
+    if (xcur[0][0][0] == 1.2345e-30f) p.mrf[0] = xcur[WM - 1][WN - 1][15];
     return;
   }
   const __amdgpu_buffer_rsrc_t mrs = __builtin_amdgcn_make_buffer_rsrc(
@@ -453,47 +479,59 @@ resblock_bf16x3(const RbParams p) {
   // divisions for every tile; the empty asm keeps the compiler from sinking a tile's loads
   // into its store branch (which serialised one HBM round trip per element)
   if (add) {
-    float mv[WN][16];
+    float mv[WM][WN][16];
 #pragma unroll
-    for (int k = 0; k < WN; ++k)
+    for (int i = 0; i < WM; ++i)
 #pragma unroll
-      for (int r = 0; r < 16; ++r)
-        mv[k][r] = __builtin_bit_cast(
-            float, __builtin_amdgcn_raw_buffer_load_b32(mrs, (int)vo[k], (int)srow(r), 0));
+      for (int k = 0; k < WN; ++k)
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          mv[i][k][r] = __builtin_bit_cast(
+              float, __builtin_amdgcn_raw_buffer_load_b32(mrs, (int)vo[k], (int)srow(i, r), 0));
 #if HFG_RB_TIMING
     wait_vm<0>();
     stamp(23);
 #endif
 #pragma unroll
-    for (int k = 0; k < WN; ++k)
+    for (int i = 0; i < WM; ++i)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) xcur[k][r] = mv[k][r] + xcur[k][r];
+      for (int k = 0; k < WN; ++k)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) xcur[i][k][r] = mv[i][k][r] + xcur[i][k][r];
   }
   if (div && p.mrf_rcp != 0.f) {
 #pragma unroll
-    for (int k = 0; k < WN; ++k)
+    for (int i = 0; i < WM; ++i)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) xcur[k][r] = div_fast(xcur[k][r], p.mrf_div, p.mrf_rcp);
+      for (int k = 0; k < WN; ++k)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) xcur[i][k][r] = div_fast(xcur[i][k][r], p.mrf_div, p.mrf_rcp);
   } else if (div) {
 #pragma unroll
-    for (int k = 0; k < WN; ++k)
+    for (int i = 0; i < WM; ++i)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) xcur[k][r] = xcur[k][r] / p.mrf_div;
+      for (int k = 0; k < WN; ++k)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) xcur[i][k][r] = xcur[i][k][r] / p.mrf_div;
   }
 #pragma unroll
-  for (int k = 0; k < WN; ++k)
+  for (int i = 0; i < WM; ++i)
 #pragma unroll
-    for (int r = 0; r < 16; ++r) asm volatile("" ::"v"(xcur[k][r]));
+    for (int k = 0; k < WN; ++k)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) asm volatile("" ::"v"(xcur[i][k][r]));
 #pragma unroll
   for (int k = 0; k < WN; ++k) {
     if (ok[k]) {
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        // through a scalar: __builtin_bit_cast of an ext_vector element lvalue compiled to
-        // element 0 of the vector (every row stored the same value)
-        const float v = xcur[k][r];
-        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), mrs, (int)vo[k], (int)srow(r), 0);
-      }
+      for (int i = 0; i < WM; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          // through a scalar: __builtin_bit_cast of an ext_vector element lvalue compiled to
+          // element 0 of the vector (every row stored the same value)
+          const float v = xcur[i][k][r];
+          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), mrs, (int)vo[k], (int)srow(i, r), 0);
+        }
     }
   }
   stamp(3 + 2 * n_conv);
@@ -509,7 +547,9 @@ resblock_bf16x3(const RbParams p) {
     for (int k = 0; k < WN; ++k) {
       float mk = 0.f;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) mk = fmaxf(mk, fabsf(xcur[k][r]));
+      for (int i = 0; i < WM; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) mk = fmaxf(mk, fabsf(xcur[i][k][r]));
       m = ok[k] ? fmaxf(m, mk) : m;
     }
     amax_commit(m, p.amax_out, b);
@@ -521,69 +561,71 @@ namespace {
 typedef void (*RbFn)(const RbParams);
 
 struct EntryRb {
-  int kt, waves_m, waves_n, np, fmt;
+  int kt, waves_m, waves_n, wm, np, fmt;
   RbFn fn;
   char name[64];
+  int C() const { return 32 * wm * waves_m; }
+  int nwin() const { return 32 * (4 / wm) * waves_n; }
 };
 
-#define HFGRB_ENTRY(KT, WMS, WNS, NP, FMT) \
-  { KT, WMS, WNS, NP, FMT, resblock_bf16x3<KT, WMS, WNS, NP, FMT>, {0} }
-#define HFGRB_KTS(WMS, WNS, NP, FMT)                                                  \
-  HFGRB_ENTRY(3, WMS, WNS, NP, FMT), HFGRB_ENTRY(5, WMS, WNS, NP, FMT),               \
-      HFGRB_ENTRY(7, WMS, WNS, NP, FMT), HFGRB_ENTRY(11, WMS, WNS, NP, FMT)
-// C = 64 (2 x 4 waves), C = 32 (1 x 4), C = 128 (4 x 2, k = 3), C = 64 narrow (2 x 2, k = 3)
-#define HFGRB_SET(NP, FMT)                                                            \
-  HFGRB_KTS(2, 4, NP, FMT), HFGRB_KTS(1, 4, NP, FMT), HFGRB_ENTRY(3, 4, 2, NP, FMT),   \
-      HFGRB_ENTRY(3, 2, 2, NP, FMT)
+#define HFGRB_ENTRY(KT, WMS, WNS, WM, NP, FMT) \
+  { KT, WMS, WNS, WM, NP, FMT, resblock_bf16x3<KT, WMS, WNS, WM, NP, FMT>, {0} }
+#define HFGRB_KTS(WMS, WNS, WM, NP, FMT)                                                   \
+  HFGRB_ENTRY(3, WMS, WNS, WM, NP, FMT), HFGRB_ENTRY(5, WMS, WNS, WM, NP, FMT),            \
+      HFGRB_ENTRY(7, WMS, WNS, WM, NP, FMT), HFGRB_ENTRY(11, WMS, WNS, WM, NP, FMT)
+// 32-row waves (WM 1): C = 64 (2 x 4 waves), C = 32 (1 x 4), C = 128 (4 x 2, k = 3),
+// C = 64 narrow (2 x 2, k = 3).  64-row waves (WM 2: half the LDS operand reads per MFMA,
+// twice the weight-fragment loads) measured the same in a same-box A/B (round 4) and are not
+// instantiated.
+#define HFGRB_SET(NP, FMT)                                                                 \
+  HFGRB_KTS(2, 4, 1, NP, FMT), HFGRB_KTS(1, 4, 1, NP, FMT), HFGRB_ENTRY(3, 4, 2, 1, NP, FMT), \
+      HFGRB_ENTRY(3, 2, 2, 1, NP, FMT)
 
 // bf16x3 (NP 3, bf16), f16x3 (NP 3, f16), bf16w (NP 2 on the f16 kernels)
 EntryRb g_entriesRb[] = {HFGRB_SET(3, 0), HFGRB_SET(3, 1), HFGRB_SET(2, 1)};
 
-}  // namespace
-
-bool rb_supported(int C, int kt, int waves_n) {
-  if (kt != 3 && kt != 5 && kt != 7 && kt != 11) return false;
-  const int wm = C / 32;
-  if (C % 32 != 0) return false;
+EntryRb* find_rb(int C, int nwin, int wm, int kt, int np, int fmt) {
   for (auto& e : g_entriesRb)
-    if (e.kt == kt && e.waves_m == wm && e.waves_n == waves_n && e.np == 3 && e.fmt == 0) return true;
-  return false;
+    if (e.kt == kt && e.C() == C && e.nwin() == nwin && e.wm == wm && e.np == np && e.fmt == fmt)
+      return &e;
+  return nullptr;
 }
 
-size_t rb_lds_bytes(int C, int waves_n, int n_conv) {
-  const size_t rows = (size_t)kRbColsPerWave * waves_n + 2 * rb_marg(C, waves_n);
+}  // namespace
+
+bool rb_supported(int C, int kt, int nwin, int wm) {
+  return find_rb(C, nwin, wm, kt, 3, 0) != nullptr;
+}
+
+size_t rb_lds_bytes(int C, int nwin, int n_conv) {
+  const size_t rows = (size_t)nwin + 2 * rb_marg(C, nwin);
   // operand planes, biases, the per-wave maxima of f16x3 (<= 16 waves)
   return (size_t)C * rows * 4 + sizeof(float) * ((size_t)n_conv * C + 16);
 }
 
-hipError_t launch_resblock_bf16x3(int C, int waves_n, int kt, int fmt, int np, const RbParams& p,
-                                  int batch, hipStream_t stream, const char** name) {
-  const int wm = C / 32;
-  EntryRb* e = nullptr;
-  for (auto& cand : g_entriesRb)
-    if (cand.kt == kt && cand.waves_m == wm && cand.waves_n == waves_n && cand.np == np &&
-        cand.fmt == fmt)
-      e = &cand;
-  if (!e || C % 32 != 0) return hipErrorInvalidValue;
-  const int nwin = kRbColsPerWave * waves_n;
+hipError_t launch_resblock_bf16x3(int C, int nwin, int wm, int kt, int fmt, int np,
+                                  const RbParams& p, int batch, hipStream_t stream,
+                                  const char** name) {
+  EntryRb* e = find_rb(C, nwin, wm, kt, np, fmt);
+  if (!e) return hipErrorInvalidValue;
   if (p.n_conv < 2 || p.n_conv > kRbMaxConv || (p.n_conv & 1)) return hipErrorInvalidValue;
   if (p.conv0 < 0 || p.conv0 + p.n_conv > p.n_conv_stream) return hipErrorInvalidValue;
   if (p.W <= 0 || p.halo < 0 || p.W + 2 * p.halo > nwin) return hipErrorInvalidValue;
   for (int i = 0; i < p.n_conv; ++i)
-    if (p.dil[i] < 1 || (kt - 1) / 2 * p.dil[i] > rb_marg(C, waves_n)) return hipErrorInvalidValue;
+    if (p.dil[i] < 1 || (kt - 1) / 2 * p.dil[i] > rb_marg(C, nwin)) return hipErrorInvalidValue;
   {
     std::lock_guard<std::mutex> lk(setup_mutex());
     if (!e->name[0])
-      snprintf(e->name, sizeof(e->name), "resblock_bf16x3<%d, %d, %d, %d, %d>", e->kt, e->waves_m,
-               e->waves_n, e->np, e->fmt);
+      snprintf(e->name, sizeof(e->name), "resblock_bf16x3<%d, %d, %d, %d, %d, %d>", e->kt,
+               e->waves_m, e->waves_n, e->wm, e->np, e->fmt);
   }
-  const size_t lds = rb_lds_bytes(C, waves_n, p.n_conv);
+  const size_t lds = rb_lds_bytes(C, nwin, p.n_conv);
   if (lds > 160 * 1024) return hipErrorInvalidValue;
   if (hipError_t err = ensure_max_lds(reinterpret_cast<const void*>(e->fn)))
     return err;
   if (name) *name = e->name;
   const int n_tiles = (p.L + p.W - 1) / p.W;
-  e->fn<<<dim3(n_tiles, batch), dim3(64 * wm * waves_n), lds, stream>>>(p);
+  e->fn<<<dim3(n_tiles, batch), dim3(64 * e->waves_m * e->waves_n), lds, stream>>>(p);
   return hipGetLastError();
 }
 
