@@ -400,6 +400,15 @@ conv1d_bf16x3(const ConvParams p) {
 #else
   auto cstamp = [](int) {};
 #endif
+  // AREG: the m-tile's bias in LDS for the epilogue (conv_epilogue_lds2), visible after the
+  // prologue barrier
+  static_assert(!AREG || (WAVES_M == kBf16x3Tiles[5].WAVES_M && WAVES_N == kBf16x3Tiles[5].WAVES_N &&
+                          WM == kBf16x3Tiles[5].WM && WN == kBf16x3Tiles[5].WN),
+                "AREG = tile 5 (the host sizes its LDS from that configuration)");
+  constexpr int BIAS_OFF = AREG ? bf16x3_areg_bias_off(KT_MAX, kBf16x3Tiles[5]) : 0;
+  float* const bias_lds = reinterpret_cast<float*>(reinterpret_cast<char*>(lds16) + BIAS_OFF);
+  if constexpr (AREG)
+    for (int i = tid; i < MT; i += NT) bias_lds[i] = p.bias[mt * MT + i];
   // ---- prologue: weight slabs of chunks 0..WD-2, input window of channel group 0 ----
   load_x(0);
   if constexpr (!AREG) {
@@ -787,8 +796,13 @@ conv1d_bf16x3(const ConvParams p) {
       lds_barrier();
       cstamp(7);
       float* stage = reinterpret_cast<float*>(lds16) + wave * 32 * (32 * WN + 8);
-      conv_epilogue_lds<WM, WN>(p, acc, b, mt * MT + wave_m * 32 * WM, n0 + wave_n * 32 * WN,
-                                N_b, half, col, stage, lane, sc);
+      if constexpr (AREG)
+        conv_epilogue_lds2<WM, WN>(p, acc, b, mt * MT + wave_m * 32 * WM, mt * MT,
+                                   n0 + wave_n * 32 * WN, N_b, half, col, stage, bias_lds, lane,
+                                   sc);
+      else
+        conv_epilogue_lds<WM, WN>(p, acc, b, mt * MT + wave_m * 32 * WM, n0 + wave_n * 32 * WN,
+                                  N_b, half, col, stage, lane, sc);
     } else {
       conv_epilogue<WM, WN>(p, acc, b, mt * MT + wave_m * 32 * WM, n0 + wave_n * 32 * WN, N_b,
                             half, col, sc);
@@ -880,6 +894,8 @@ hipError_t launch_conv_bf16x3(int tile, int kt, bool ups, int fmt, int np, const
   size_t lds = bf16x3_lds_bytes(tile, kt, p.dil);
   if (p.epi_lds && !ups)
     lds = std::max(lds, (size_t)t.threads() / 64 * 32 * (32 * t.WN + 8) * sizeof(float));
+  // AREG: + the m-tile's bias copy (its kernel instance is compiled for its KT)
+  if (t.AREG) lds = (size_t)bf16x3_areg_bias_off(e->kt, t) + (size_t)t.MT() * sizeof(float);
   if (lds > 160 * 1024) return hipErrorInvalidValue;
   if (hipError_t err = ensure_max_lds(reinterpret_cast<const void*>(e->fn)))
     return err;

@@ -12,12 +12,25 @@
 #include <hip/hip_runtime.h>
 
 #include <type_traits>
+#include <utility>
 
 #include "kernels.h"
 
 namespace hfg {
 
 typedef float floatx16e __attribute__((ext_vector_type(16)));
+
+// f(integral_constant<int, 0>) ... f(integral_constant<int, N - 1>): a compile-time loop (a
+// `#pragma unroll` loop around a large body can stay a loop, and an accumulator array it
+// indexes then lives in scratch)
+template <typename F, int... Is>
+__device__ __forceinline__ void static_for_impl(F& f, std::integer_sequence<int, Is...>) {
+  (f(std::integral_constant<int, Is>{}), ...);
+}
+template <int N, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+  static_for_impl(f, std::make_integer_sequence<int, N>{});
+}
 
 // largest value over a wave (every lane active): DPP max within each 16-lane row (quad swaps,
 // then row rotations by 4 and 8), then the 4 row maxima by readlane — a few cycles per step,
@@ -284,6 +297,133 @@ __device__ __forceinline__ void conv_epilogue_lds(const ConvParams& p, floatx16e
     }
     __builtin_amdgcn_wave_barrier();
   }
+  if (p.amax_out) amax_commit(vmax, p.amax_out, b);
+}
+
+// conv_epilogue_lds with the m-tile's bias in LDS (bias_lds[row - m-tile origin], copied at
+// kernel start): vmcnt counts loads and stores in one in-order queue, so a global load issued
+// after a store cannot complete for the wave before that store has; the per-float4 bias loads
+// of conv_epilogue_lds each waited for the stores before them.  Here the only global loads are
+// the residual / MRF batches, every one issued before the batch's stores (the whole row tile
+// with one of them, half of it with both: register budget).
+template <int WM, int WN>
+__device__ __forceinline__ void conv_epilogue_lds2(const ConvParams& p, floatx16e (&acc)[WM][WN],
+                                                   int b, int row_base, int row_tile0, int n_base,
+                                                   int N_b, int half, int col, float* stage,
+                                                   const float* bias_lds, int lane, float sc) {
+  constexpr int SROW = 32 * WN + 8;
+  constexpr int C4 = 8 * WN;                 // float4 per staged row
+  constexpr int IT = 32 * C4 / 64;           // float4 per lane and row tile
+  const int64_t bo = (int64_t)b * p.y_bs;
+  const float* resb = p.res ? p.res + bo : nullptr;
+  float* outb = (p.mrf ? p.mrf : p.y) + bo;
+  const bool add_mrf = p.mrf && (p.mrf_mode & 1);
+  const bool div_mrf = p.mrf && (p.mrf_mode & 2);
+  const bool act = p.act_out != 0;
+  float vmax = 0.f;  // max |stored value| (f16x3 consumers: p.amax_out)
+  static_for<WM>([&](auto i_tag) {
+    constexpr int i = decltype(i_tag)::value;
+#pragma unroll
+    for (int k = 0; k < WN; ++k)
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        stage[((r & 3) + 8 * (r >> 2) + 4 * half) * SROW + k * 32 + col] = acc[i][k][r];
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's writes are in LDS
+    __builtin_amdgcn_wave_barrier();
+    auto batch = [&](auto bs_tag, auto r_tag, auto m_tag, auto u0_tag) {
+      constexpr int BS = decltype(bs_tag)::value, U0 = decltype(u0_tag)::value;
+      constexpr bool R = decltype(r_tag)::value, M = decltype(m_tag)::value;
+      float4 rv[BS], mv[BS];
+      static_for<BS>([&](auto j_tag) {
+        constexpr int j = decltype(j_tag)::value;
+        const int e = (U0 + j) * 64 + lane;
+        const int rr = e / C4, c4 = e - rr * C4;
+        const int row = row_base + i * 32 + rr, n = n_base + 4 * c4;
+        const bool ok = row < p.M && n < N_b;
+        const int64_t o = (int64_t)row * p.N + n;
+        if constexpr (R)
+          rv[j] = ok ? *reinterpret_cast<const float4*>(resb + o) : float4{0.f, 0.f, 0.f, 0.f};
+        if constexpr (M)
+          mv[j] = ok ? *reinterpret_cast<const float4*>(outb + o) : float4{0.f, 0.f, 0.f, 0.f};
+      });
+      static_for<BS>([&](auto j_tag) {
+        constexpr int j = decltype(j_tag)::value;
+        const int e = (U0 + j) * 64 + lane;
+        const int rr = e / C4, c4 = e - rr * C4;
+        const int row = row_base + i * 32 + rr, n = n_base + 4 * c4;
+        const bool ok = row < p.M && n < N_b;
+        const bool full = ok && n + 3 < N_b;
+        float4 v = *reinterpret_cast<const float4*>(stage + rr * SROW + 4 * c4);
+        const float bv = bias_lds[row - row_tile0];
+        v.x = __builtin_fmaf(v.x, sc, bv);
+        v.y = __builtin_fmaf(v.y, sc, bv);
+        v.z = __builtin_fmaf(v.z, sc, bv);
+        v.w = __builtin_fmaf(v.w, sc, bv);
+        if constexpr (R) {
+          v.x = rv[j].x + v.x;
+          v.y = rv[j].y + v.y;
+          v.z = rv[j].z + v.z;
+          v.w = rv[j].w + v.w;
+        }
+        if (act) {
+          v.x = v.x > 0.f ? v.x : v.x * kLReluSlope;
+          v.y = v.y > 0.f ? v.y : v.y * kLReluSlope;
+          v.z = v.z > 0.f ? v.z : v.z * kLReluSlope;
+          v.w = v.w > 0.f ? v.w : v.w * kLReluSlope;
+        }
+        if constexpr (M) {
+          v.x = mv[j].x + v.x;
+          v.y = mv[j].y + v.y;
+          v.z = mv[j].z + v.z;
+          v.w = mv[j].w + v.w;
+        }
+        if (div_mrf) {
+          v.x = v.x / p.mrf_div;
+          v.y = v.y / p.mrf_div;
+          v.z = v.z / p.mrf_div;
+          v.w = v.w / p.mrf_div;
+        }
+        if (p.amax_out) {
+          // the stored elements only: a partial quad's tail past N_b is not written
+          if (full) {
+            vmax = fmaxf(vmax, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+          } else if (ok) {
+            const int nv = N_b - n;
+            vmax = fmaxf(vmax, fabsf(v.x));
+            if (nv > 1) vmax = fmaxf(vmax, fabsf(v.y));
+            if (nv > 2) vmax = fmaxf(vmax, fabsf(v.z));
+          }
+        }
+        float* dst = outb + (int64_t)row * p.N + n;
+        if (full) {
+          // streamed once (the next launch reads it from HBM / MALL): non-temporal
+          typedef float f4v __attribute__((ext_vector_type(4)));
+          const f4v nv = {v.x, v.y, v.z, v.w};
+          __builtin_nontemporal_store(nv, reinterpret_cast<f4v*>(dst));
+        } else if (ok) {
+          dst[0] = v.x;
+          if (n + 1 < N_b) dst[1] = v.y;
+          if (n + 2 < N_b) dst[2] = v.z;
+        }
+      });
+    };
+    using T_ = std::true_type;
+    using F_ = std::false_type;
+    using IFull = std::integral_constant<int, IT>;
+    using IHalf = std::integral_constant<int, IT / 2>;
+    using Z = std::integral_constant<int, 0>;
+    if (resb && add_mrf) {  // block-uniform branches
+      batch(IHalf{}, T_{}, T_{}, Z{});
+      batch(IHalf{}, T_{}, T_{}, IHalf{});
+    } else if (resb) {
+      batch(IFull{}, T_{}, F_{}, Z{});
+    } else if (add_mrf) {
+      batch(IFull{}, F_{}, T_{}, Z{});
+    } else {
+      batch(IFull{}, F_{}, F_{}, Z{});
+    }
+    __builtin_amdgcn_wave_barrier();
+  });
   if (p.amax_out) amax_commit(vmax, p.amax_out, b);
 }
 

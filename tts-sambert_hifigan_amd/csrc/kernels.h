@@ -164,6 +164,13 @@ constexpr int bf16x3_areg_rows(int kt, const Bf16x3Cfg& t) {
   const int nt = t.threads();
   return (2 * xw_max + nt - 1) / nt * nt / 2;
 }
+// AREG tile: byte offset of the m-tile's bias copy in LDS (read by the LDS-staged epilogue:
+// no global load between its stores) = past both the input planes and the epilogue staging
+constexpr int bf16x3_areg_bias_off(int kt, const Bf16x3Cfg& t) {
+  const int xbytes = 2 * 4 * (bf16x3_areg_rows(kt, t) * 16 + 64);
+  const int stage = t.threads() / 64 * 32 * (32 * t.WN + 8) * 4;
+  return ((xbytes > stage ? xbytes : stage) + 15) & ~15;
+}
 inline int bf16x3_tile_for_rows(int M) { return M >= 128 ? 3 : (M >= 64 ? 1 : (M >= 32 ? 2 : -1)); }
 size_t bf16x3_lds_bytes(int tile, int kt, int dil);
 // the bf16x3 layer kernel handles kt taps at dilation dil (else the fp32 kernel runs)

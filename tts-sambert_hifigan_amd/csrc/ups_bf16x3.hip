@@ -27,8 +27,8 @@
 //   * B (lrelu'd, split input): the window of frames [m0-4, m0+NTILE+4) (quad-aligned, so
 //     every load is one 16-B dwordx4: 4 frames of one channel) is loaded one group ahead into
 //     registers, converted after the group's MFMAs and written as [frame][16 ch] bf16 hi / lo
-//     planes (16-B halves XOR-swizzled by (frame>>3)&1: conflict-free ds_read_b128 for the
-//     three tap offsets -1, 0, +1).
+//     planes (16-B slots XOR-swizzled per 256-B block, xrow_off: conflict-free ds_read_b128
+//     for the three tap offsets -1, 0, +1, and staging writes within their transfer cycles).
 #include <hip/hip_runtime.h>
 
 #include <mutex>
@@ -76,6 +76,15 @@ ups_bf16x3(const UpsParams p) {
   constexpr int PW = SLAB / 1024 / NW;       // LDS-DMA pieces per thread per slab
   static_assert(PW * 1024 * NW == SLAB, "slab must split evenly over the waves");
 
+  // byte offset of (frame row r, 8-channel half h) in a staged plane: the 16-B slot 2r + h
+  // XOR-swizzled inside its 256-B block by bits 2-3 of r.  The B reads (16 consecutive rows of
+  // one half per 16-lane group) stay conflict-free, and so do the staging writes (8 lanes =
+  // 4 quads x 2 halves, task order below), which the unswizzled layout put on 2 of the 8 16-B
+  // slots of a bank window (1.2 conflict cycles per LDS-active cycle; bank model
+  // tests/tools/ups_lds_banks.py)
+  auto xrow_off = [](int r, int h) {
+    return 16 * ((2 * r + h) ^ (((r >> 3) & 1) * 5 + ((r >> 2) & 1) * 2));
+  };
   extern __shared__ __attribute__((aligned(16))) char lds[];
   char* const Abuf = lds;                    // 2 slabs
   char* const Xbuf = lds + 2 * SLAB;         // 2 x (hi, lo) planes
@@ -133,8 +142,10 @@ ups_bf16x3(const UpsParams p) {
   const int grp_rec = (int)(unsigned)(grp_bytes < 0xFFFFFFFFll ? grp_bytes : 0xFFFFFFFFll);
   const int task = wave * TPW + lane;
   const bool has_task = lane < TPW && task < NTASK;
-  const int hf = task / NQ;                  // channel half of the task
-  const int xq = task - hf * NQ;             // quad of the task
+  // (quad, half) interleaved: the 8 lanes of a ds_write_b128 group write 4 quads x both
+  // halves, which xrow_off's swizzle puts on the 8 distinct 16-B slots of a bank window
+  const int hf = task & 1;                   // channel half of the task
+  const int xq = task >> 1;                  // quad of the task
   const int t0 = m0 - 4 + 4 * xq;            // first frame of the quad
   // leaky_relu as max(v * sx, v * 0.1 sx) (f16x3 scale sx; bitwise max(v, 0.1 v) for bf16x3)
   // and the zero padding as a select: frames in [T_b, L) of a ragged item were never written
@@ -157,51 +168,17 @@ ups_bf16x3(const UpsParams p) {
       xv[e] = __builtin_bit_cast(
           f4, __builtin_amdgcn_raw_buffer_load_b128(xrs, (int)xoff_lane, e * xcs4, 0));
   };
-  // The 8 lanes of a ds_write_b128 lane group hold 8 consecutive quads xq; writing frame tt
-  // of each quad at once put them on 2 of the 8 16-B bank groups (the row offset mod 128 B is
-  // tt * 32 + the half swizzle): a 4-way conflict (SQ: 1.2 / 1.49 bank-conflict cycles per
-  // LDS-active cycle).  HFG_UPS_ROT: lane xq writes its frames in the order
-  // tt = (j + g) & 3, g = (xq & 1) + ((xq >> 1) & 2) — with the swizzle bit (xq >> 1) & 1 the
-  // 8 lanes then cover all 8 bank groups (profiles/r04 bank model) — and the frames are
-  // rotated in registers by g first (2 selects per value); the layout and the readers are
-  // unchanged.
-#ifndef HFG_UPS_ROT
-#define HFG_UPS_ROT 0
-#endif
   auto store_x = [&](int buf) {
     if (!has_task) return;
     char* xh = Xbuf + buf * XBUF;
-    const int g = HFG_UPS_ROT ? (xq & 1) + ((xq >> 1) & 2) : 0;
-    f4 xr[8];
-    bool okr[4];
-#pragma unroll
-    for (int e = 0; e < 8; ++e) xr[e] = xv[e];
-#pragma unroll
-    for (int tt = 0; tt < 4; ++tt) okr[tt] = okt[tt];
-    if (HFG_UPS_ROT) {
-      const bool b0 = g & 1, b1 = g & 2;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        f4 y;
-#pragma unroll
-        for (int tt = 0; tt < 4; ++tt) y[tt] = b0 ? xr[e][(tt + 1) & 3] : xr[e][tt];
-#pragma unroll
-        for (int tt = 0; tt < 4; ++tt) xr[e][tt] = b1 ? y[(tt + 2) & 3] : y[tt];
-      }
-      bool oy[4];
-#pragma unroll
-      for (int tt = 0; tt < 4; ++tt) oy[tt] = b0 ? okr[(tt + 1) & 3] : okr[tt];
-#pragma unroll
-      for (int tt = 0; tt < 4; ++tt) okr[tt] = b1 ? oy[(tt + 2) & 3] : oy[tt];
-    }
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       bf16x8 hv, lv;
 #pragma unroll
       for (int e = 0; e < 8; e += 2) {
         floatx2 a;
-        a[0] = okr[j] ? fmaxf(xr[e][j] * sx, xr[e][j] * sx1) : 0.f;
-        a[1] = okr[j] ? fmaxf(xr[e + 1][j] * sx, xr[e + 1][j] * sx1) : 0.f;
+        a[0] = okt[j] ? fmaxf(xv[e][j] * sx, xv[e][j] * sx1) : 0.f;
+        a[1] = okt[j] ? fmaxf(xv[e + 1][j] * sx, xv[e + 1][j] * sx1) : 0.f;
         bf16x2 hh, ll;
         split2<FMT>(a, hh, ll);
         hv[e] = hh[0];
@@ -209,8 +186,7 @@ ups_bf16x3(const UpsParams p) {
         lv[e] = ll[0];
         lv[e + 1] = ll[1];
       }
-      const int r = 4 * xq + ((j + g) & 3);
-      const int off = r * 32 + 16 * (hf ^ ((r >> 3) & 1));
+      const int off = xrow_off(4 * xq + j, hf);
       *reinterpret_cast<bf16x8*>(xh + off) = hv;
       *reinterpret_cast<bf16x8*>(xh + XPLANE + off) = lv;
     }
@@ -261,8 +237,7 @@ ups_bf16x3(const UpsParams p) {
       bf16x8 bh[3], bl[3];
 #pragma unroll
       for (int o = 0; o < 3; ++o) {
-        const int r = colw + 32 * k + o - 1;
-        const int off = r * 32 + 16 * (half ^ ((r >> 3) & 1));
+        const int off = xrow_off(colw + 32 * k + o - 1, half);
         bh[o] = *reinterpret_cast<const bf16x8*>(xh + off);
         bl[o] = *reinterpret_cast<const bf16x8*>(xh + XPLANE + off);
       }
