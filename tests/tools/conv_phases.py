@@ -68,6 +68,11 @@ def main():
                "barrier_wait": int(np.median(blk[:, 5])),
                "epilogue": int(np.median(blk[:, 4] - blk[:, 3])),
                "epi_wait_barrier": int(np.median(blk[:, 7] - blk[:, 3])),
+               "epi_stage0": int(np.median(blk[:, 8] - blk[:, 7])),
+               "epi_tile0": int(np.median(blk[:, 9] - blk[:, 8])),
+               "epi_stage1": int(np.median(blk[:, 10] - blk[:, 9])),
+               "epi_tile1": int(np.median(blk[:, 11] - blk[:, 10])),
+               "epi_commit": int(np.median(blk[:, 4] - blk[:, 11])),
                "start_spread_us": [round(float(np.percentile(starts - starts[0], q)) / 100.0, 1)
                                    for q in (25, 50, 75, 100)]}
         out[f"k{kt} {epi}"] = row

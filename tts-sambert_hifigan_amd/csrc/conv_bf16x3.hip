@@ -390,12 +390,12 @@ conv1d_bf16x3(const ConvParams p) {
                                            (p.res ? ((p.mrf && (p.mrf_mode & 1)) ? 2 : 1) : 0)) * kCvTsBlocks +
                                    ((blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x) % kCvTsBlocks) *
                                       kCvTsSlots;
-  auto cstamp = [&](int i) {
-    const uint64_t t = __builtin_amdgcn_s_memtime();
-    if (AREG && tid == 0) cts[i] = t;
-  };
+  // stamps kept in SGPRs and stored once at the end: a stamp store mid-kernel would make
+  // every later vmcnt wait also wait for its write (one in-order queue for loads and stores)
+  uint64_t tsv[16] = {};
+  auto cstamp = [&](int i) { tsv[i] = __builtin_amdgcn_s_memtime(); };
   uint64_t bar_wait = 0;
-  if (AREG && tid == 0) cts[0] = __builtin_amdgcn_s_memrealtime();
+  tsv[0] = __builtin_amdgcn_s_memrealtime();
   cstamp(1);
 #else
   auto cstamp = [](int) {};
@@ -552,7 +552,7 @@ conv1d_bf16x3(const ConvParams p) {
 #endif
     }
 #if HFG_CONV_TIMING
-    if (tid == 0) cts[5] = bar_wait;
+    tsv[5] = bar_wait;
 #endif
     cstamp(3);
   } else if constexpr (KT_ > 0 && WM * WN >= 8) {
@@ -799,7 +799,11 @@ conv1d_bf16x3(const ConvParams p) {
       if constexpr (AREG)
         conv_epilogue_lds2<WM, WN>(p, acc, b, mt * MT + wave_m * 32 * WM, mt * MT,
                                    n0 + wave_n * 32 * WN, N_b, half, col, stage, bias_lds, lane,
+#if HFG_CONV_TIMING
+                                   sc, tsv);
+#else
                                    sc);
+#endif
       else
         conv_epilogue_lds<WM, WN>(p, acc, b, mt * MT + wave_m * 32 * WM, n0 + wave_n * 32 * WN,
                                   N_b, half, col, stage, lane, sc);
@@ -810,7 +814,10 @@ conv1d_bf16x3(const ConvParams p) {
   }
   cstamp(4);
 #if HFG_CONV_TIMING
-  if (AREG && tid == 0) cts[6] = __builtin_amdgcn_s_memrealtime();
+  tsv[6] = __builtin_amdgcn_s_memrealtime();
+  if (AREG && tid == 0)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) cts[i] = tsv[i];
 #endif
 }
 

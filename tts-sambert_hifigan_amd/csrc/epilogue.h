@@ -310,7 +310,13 @@ template <int WM, int WN>
 __device__ __forceinline__ void conv_epilogue_lds2(const ConvParams& p, floatx16e (&acc)[WM][WN],
                                                    int b, int row_base, int row_tile0, int n_base,
                                                    int N_b, int half, int col, float* stage,
-                                                   const float* bias_lds, int lane, float sc) {
+                                                   const float* bias_lds, int lane, float sc,
+                                                   uint64_t* tsv = nullptr) {
+  // tsv (clock-stamp diagnostic builds): row tile i's staging done -> tsv[8 + 2i], its stores
+  // issued -> tsv[9 + 2i] (registers: the caller stores them at the end)
+  auto ts = [&](int s_) {
+    if (tsv) tsv[s_] = __builtin_amdgcn_s_memtime();
+  };
   constexpr int SROW = 32 * WN + 8;
   constexpr int C4 = 8 * WN;                 // float4 per staged row
   constexpr int IT = 32 * C4 / 64;           // float4 per lane and row tile
@@ -330,10 +336,18 @@ __device__ __forceinline__ void conv_epilogue_lds2(const ConvParams& p, floatx16
         stage[((r & 3) + 8 * (r >> 2) + 4 * half) * SROW + k * 32 + col] = acc[i][k][r];
     __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's writes are in LDS
     __builtin_amdgcn_wave_barrier();
+    ts(8 + 2 * i);
+    // wave-uniform: the whole 32 x 32*WN tile of this row tile lies inside [0, M) x [0, N_b)
+    // -> unmasked float4 stores (the masked path branches per element)
+    const bool interior = __builtin_amdgcn_readfirstlane(row_base) + i * 32 + 31 < p.M &&
+                          __builtin_amdgcn_readfirstlane(n_base) + 32 * WN - 1 < N_b;
     auto batch = [&](auto bs_tag, auto r_tag, auto m_tag, auto u0_tag) {
       constexpr int BS = decltype(bs_tag)::value, U0 = decltype(u0_tag)::value;
       constexpr bool R = decltype(r_tag)::value, M = decltype(m_tag)::value;
-      float4 rv[BS], mv[BS];
+      float4 rv[BS], mv[BS], sv[BS];
+      float bv[BS];
+      // global loads first, then every LDS read of the batch (one latency each, not one per
+      // float4), then the arithmetic and the stores
       static_for<BS>([&](auto j_tag) {
         constexpr int j = decltype(j_tag)::value;
         const int e = (U0 + j) * 64 + lane;
@@ -350,15 +364,19 @@ __device__ __forceinline__ void conv_epilogue_lds2(const ConvParams& p, floatx16
         constexpr int j = decltype(j_tag)::value;
         const int e = (U0 + j) * 64 + lane;
         const int rr = e / C4, c4 = e - rr * C4;
+        sv[j] = *reinterpret_cast<const float4*>(stage + rr * SROW + 4 * c4);
+        bv[j] = bias_lds[row_base + i * 32 + rr - row_tile0];
+      });
+      static_for<BS>([&](auto j_tag) {
+        constexpr int j = decltype(j_tag)::value;
+        const int e = (U0 + j) * 64 + lane;
+        const int rr = e / C4, c4 = e - rr * C4;
         const int row = row_base + i * 32 + rr, n = n_base + 4 * c4;
-        const bool ok = row < p.M && n < N_b;
-        const bool full = ok && n + 3 < N_b;
-        float4 v = *reinterpret_cast<const float4*>(stage + rr * SROW + 4 * c4);
-        const float bv = bias_lds[row - row_tile0];
-        v.x = __builtin_fmaf(v.x, sc, bv);
-        v.y = __builtin_fmaf(v.y, sc, bv);
-        v.z = __builtin_fmaf(v.z, sc, bv);
-        v.w = __builtin_fmaf(v.w, sc, bv);
+        float4 v = sv[j];
+        v.x = __builtin_fmaf(v.x, sc, bv[j]);
+        v.y = __builtin_fmaf(v.y, sc, bv[j]);
+        v.z = __builtin_fmaf(v.z, sc, bv[j]);
+        v.w = __builtin_fmaf(v.w, sc, bv[j]);
         if constexpr (R) {
           v.x = rv[j].x + v.x;
           v.y = rv[j].y + v.y;
@@ -383,27 +401,33 @@ __device__ __forceinline__ void conv_epilogue_lds2(const ConvParams& p, floatx16
           v.z = v.z / p.mrf_div;
           v.w = v.w / p.mrf_div;
         }
-        if (p.amax_out) {
-          // the stored elements only: a partial quad's tail past N_b is not written
-          if (full) {
-            vmax = fmaxf(vmax, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
-          } else if (ok) {
-            const int nv = N_b - n;
-            vmax = fmaxf(vmax, fabsf(v.x));
-            if (nv > 1) vmax = fmaxf(vmax, fabsf(v.y));
-            if (nv > 2) vmax = fmaxf(vmax, fabsf(v.z));
-          }
-        }
         float* dst = outb + (int64_t)row * p.N + n;
+        typedef float f4v __attribute__((ext_vector_type(4)));
+        if (interior) {
+          vmax = fmaxf(vmax, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+          if (kAblate && (p.dbg & 16384)) {
+            // ablation bit 14: no stores (timing only)
+            if (v.x == 1.2345e-30f) dst[0] = v.y;
+          } else {
+            // streamed once (the next launch reads it from HBM / MALL): non-temporal
+            const f4v nv = {v.x, v.y, v.z, v.w};
+            __builtin_nontemporal_store(nv, reinterpret_cast<f4v*>(dst));
+          }
+          return;
+        }
+        const bool ok = row < p.M && n < N_b;
+        const bool full = ok && n + 3 < N_b;
+        // the stored elements only: a partial quad's tail past N_b is not written
         if (full) {
-          // streamed once (the next launch reads it from HBM / MALL): non-temporal
-          typedef float f4v __attribute__((ext_vector_type(4)));
+          vmax = fmaxf(vmax, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
           const f4v nv = {v.x, v.y, v.z, v.w};
           __builtin_nontemporal_store(nv, reinterpret_cast<f4v*>(dst));
         } else if (ok) {
+          const int nv = N_b - n;
+          vmax = fmaxf(vmax, fabsf(v.x));
           dst[0] = v.x;
-          if (n + 1 < N_b) dst[1] = v.y;
-          if (n + 2 < N_b) dst[2] = v.z;
+          if (nv > 1) vmax = fmaxf(vmax, fabsf(v.y)), dst[1] = v.y;
+          if (nv > 2) vmax = fmaxf(vmax, fabsf(v.z)), dst[2] = v.z;
         }
       });
     };
@@ -416,12 +440,15 @@ __device__ __forceinline__ void conv_epilogue_lds2(const ConvParams& p, floatx16
       batch(IHalf{}, T_{}, T_{}, Z{});
       batch(IHalf{}, T_{}, T_{}, IHalf{});
     } else if (resb) {
-      batch(IFull{}, T_{}, F_{}, Z{});
+      batch(IHalf{}, T_{}, F_{}, Z{});
+      batch(IHalf{}, T_{}, F_{}, IHalf{});
     } else if (add_mrf) {
-      batch(IFull{}, F_{}, T_{}, Z{});
+      batch(IHalf{}, F_{}, T_{}, Z{});
+      batch(IHalf{}, F_{}, T_{}, IHalf{});
     } else {
       batch(IFull{}, F_{}, F_{}, Z{});
     }
+    ts(9 + 2 * i);
     __builtin_amdgcn_wave_barrier();
   });
   if (p.amax_out) amax_commit(vmax, p.amax_out, b);

@@ -102,14 +102,17 @@ resblock_bf16x3(const RbParams p) {
                               (p.conv0 > 0 ? 1 : 0);
   const int ts_blk = blockIdx.y * gridDim.x + blockIdx.x;
   uint64_t* const ts = g_rb_ts + ((size_t)ts_region * kRbTsBlocks + (ts_blk < kRbTsBlocks ? ts_blk : 0)) * kRbTsSlots;
+  // stamps kept in LDS (past the f16x3 maxima) and stored once at the end: a global (or
+  // scratch) store mid-kernel would make every later vmcnt wait also wait for its write (one
+  // in-order queue for vector loads and stores)
+  uint64_t* const tsv = reinterpret_cast<uint64_t*>(amax_s + 16);
   auto stamp = [&](int i) {
     const uint64_t t = __builtin_amdgcn_s_memtime();
-    if (tid == 0) ts[i] = t;
+    if (tid == 0) tsv[i] = t;
   };
-  {
-    const uint64_t r = __builtin_amdgcn_s_memrealtime();
-    if (tid == 0) ts[0] = r;
-  }
+  if (tid < kRbTsSlots) tsv[tid] = 0;
+  __syncthreads();
+  if (tid == 0) tsv[0] = __builtin_amdgcn_s_memrealtime();
   stamp(1);
 #else
   auto stamp = [](int) {};
@@ -536,9 +539,9 @@ resblock_bf16x3(const RbParams p) {
   }
   stamp(3 + 2 * n_conv);
 #if HFG_RB_TIMING
-  {
-    const uint64_t r = __builtin_amdgcn_s_memrealtime();
-    if (tid == 0) ts[4 + 2 * n_conv] = r;
+  if (tid == 0) {
+    tsv[4 + 2 * n_conv] = __builtin_amdgcn_s_memrealtime();
+    for (int i = 0; i < kRbTsSlots; ++i) ts[i] = tsv[i];
   }
 #endif
   if (p.amax_out) {  // f16x3 consumers of the stage output (block-uniform branch)
@@ -619,7 +622,11 @@ hipError_t launch_resblock_bf16x3(int C, int nwin, int wm, int kt, int fmt, int 
       snprintf(e->name, sizeof(e->name), "resblock_bf16x3<%d, %d, %d, %d, %d, %d>", e->kt,
                e->waves_m, e->waves_n, e->wm, e->np, e->fmt);
   }
+#if HFG_RB_TIMING
+  const size_t lds = rb_lds_bytes(C, nwin, p.n_conv) + kRbTsSlots * 8;  // + the stamps
+#else
   const size_t lds = rb_lds_bytes(C, nwin, p.n_conv);
+#endif
   if (lds > 160 * 1024) return hipErrorInvalidValue;
   if (hipError_t err = ensure_max_lds(reinterpret_cast<const void*>(e->fn)))
     return err;
