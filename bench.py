@@ -474,6 +474,7 @@ def main():
     under_profiler = "rocprof" in os.environ.get("LD_PRELOAD", "")
     if world == 1 and not args.no_pmc and not args.pmc_child and not under_profiler:
         # before this process initialises the GPU: the passes are child processes
+        print("[bench] PMC traffic passes", file=sys.stderr, flush=True)
         pmc, pmc_note = pmc_traffic(["--preset", args.preset, "--batch", str(args.batch),
                                      "--frames", str(args.frames), "--precision", args.precision])
     assert torch.cuda.is_available(), "bench.py needs MI355X GPUs"
@@ -622,10 +623,17 @@ def main():
     rank_ms = {}  # per-rank ms/step of the value pass, per precision
     ev_median = {}  # per-step HIP-event median (ms) of the value pass, per precision
     e2e = {}
+    def progress(msg):
+        """one stderr line per phase (a long run then shows it is alive)"""
+        if rank == 0:
+            print(f"[bench] {msg}", file=sys.stderr, flush=True)
+
+    progress(f"measuring {args.precision}")
     elapsed, prof, out_len = measure(args.precision)
     alt = {}
     for prec in args.also:
         if prec != args.precision:
+            progress(f"measuring {prec}")
             alt[prec] = measure(prec)
 
     samples_total = global_batch * out_len * args.steps
@@ -803,6 +811,7 @@ def main():
         line["extra_configs"] = extra_configs(pkg, S, dev, args.precision)
     if world == 1 and not args.no_cpu_baseline:
         cfg_np = S.random_state_dict(cfg, seed=0) if sd_np is None else sd_np
+        progress("CPU baseline")
         line["cpu_baseline"] = cpu_baseline(cfg, cfg_np, T, args.cpu_budget_s)
         line["cpu_baseline"]["gpu_over_cpu"] = value / line["cpu_baseline"]["value"]
     print(json.dumps(line), flush=True)
