@@ -1642,7 +1642,7 @@ extern "C" {
 // "... src:<16 hex>": sha256 of the build inputs (csrc/, include/, flags), computed by
 // build.py and compiled in, so a loaded binary can be matched to its source tree
 const char* hfg_version(void) {
-  return "hifigan_hip 0.3.0 gfx950 fp32-mfma bf16x3-mfma src:" HFG_SRC_HASH;
+  return "hifigan_hip 0.4.0 gfx950 f16x3-mfma fp32-mfma bf16x3-mfma src:" HFG_SRC_HASH;
 }
 
 const char* hfg_last_error(void) { return g_err.c_str(); }
