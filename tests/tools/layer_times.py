@@ -26,6 +26,7 @@ def run(argv):
     ap.add_argument("--streams", type=int, default=1)
     ap.add_argument("--batch", type=int, default=8)
     ap.add_argument("--frames", type=int, default=1024)
+    ap.add_argument("--preset", default="v1")
     a = ap.parse_args(argv)
     sys.path.insert(0, ROOT)
     import torch
@@ -33,7 +34,7 @@ def run(argv):
     pkg = ge.load_package()
     import importlib
     S = importlib.import_module(ge.PKG_NAME + ".synth")
-    cfg = S.PRESETS["v1"]
+    cfg = S.PRESETS[a.preset]
     sd = {k: torch.from_numpy(v) for k, v in S.random_state_dict(cfg, seed=0).items()}
     dev = torch.device("cuda:0")
     gen = pkg.HiFiGANGenerator(**cfg.kwargs(), precision=a.precision).eval()
