@@ -168,6 +168,40 @@ def test_two_stream_split_is_bitwise_equal(pkg, precision):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("precision", ["f16x3", "bf16x3", "fp32"])
+def test_ragged_forward_ignores_workspace_contents(pkg, precision):
+    """A ragged batch never reads workspace frames past an item's length (the
+    output-frame upsampler masked them by a multiply, and 0 * NaN is NaN).  The same forward
+    on a workspace pre-filled with NaN, with +inf and with zeros gives bitwise the same wavs,
+    and every valid sample is finite."""
+    from oracle import config as C, prng
+    dev = _dev()
+    cfg = C.V1
+    sd = C.make_state_dict(cfg, seed=19)
+    B, T = 4, 300
+    mel = torch.as_tensor(prng.mel_input(29, (B, cfg.n_mels, T))).to(dev)
+    lens = torch.tensor([300, 157, 3, 242], dtype=torch.int32, device=dev)
+    gen = _gen(pkg, cfg, sd, dev, precision=precision)
+    h = gen.hip_handle(dev)
+    out_len = h.out_len(T)
+    ws_bytes = h.workspace_bytes(B, T)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    outs = []
+    for fill in (float("nan"), float("inf"), 0.0):
+        ws = torch.full((ws_bytes // 4 + 1,), fill, dtype=torch.float32, device=dev)
+        wav = torch.full((B, 1, out_len), 7.0, dtype=torch.float32, device=dev)
+        h.forward_ex(mel.data_ptr(), B, T, wav.data_ptr(), out_len, ws.data_ptr(), ws_bytes,
+                     stream, lengths_ptr=lens.data_ptr())
+        torch.cuda.synchronize()
+        outs.append(wav.cpu().numpy())
+    for i, n in enumerate(lens.tolist()):
+        valid = outs[2][i, 0, :n * 256]
+        assert np.isfinite(valid).all(), f"item {i}: non-finite valid samples"
+    assert np.array_equal(outs[0], outs[2], equal_nan=True), "NaN workspace changed the wav"
+    assert np.array_equal(outs[1], outs[2], equal_nan=True), "+inf workspace changed the wav"
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("precision,fused", [("f16x3", "1"), ("f16x3", "0"), ("bf16x3", "0")])
 def test_split_layer_kernels_run_to_run_bitwise(pkg, precision, fused, monkeypatch):
     """Repeated forwards are bitwise identical on every split layer-kernel tile (with the
