@@ -275,6 +275,47 @@ def test_ups_frames_kernel_bitwise(pkg, preset, B, T, lens, precision, monkeypat
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("precision", ["f16x3", "bf16x3"])
+@pytest.mark.parametrize("rb_split", ["1", "0"])
+def test_conv_post_fused_bitwise(pkg, precision, rb_split, monkeypatch):
+    """conv_post + tanh fused into the last C = 32 ResBlock launch (resblock_bf16x3.hip
+    conv_post_tail, the default wherever that stage runs one launch per ResBlock) gives the
+    separate conv_post4_tanh kernel's wav bit for bit: the same final x on conv_post's
+    receptive field, the same (channel, tap) fma order.  HFG_RB_CONC=0 keeps the small batch
+    on that schedule; ragged batch with whole windows past an item's end (zeroed by the
+    host's memset), both split and one-launch k = 11 ResBlocks; also against the oracle."""
+    from oracle import config as C, prng
+    dev = _dev()
+    cfg = C.V1
+    sd = C.make_state_dict(cfg, seed=53)
+    B, T, lens = 3, 48, [48, 29, 2]
+    mel_np = prng.mel_input(53, (B, cfg.n_mels, T))
+    mel = torch.as_tensor(mel_np).to(dev)
+    ln = torch.tensor(lens, dtype=torch.int32, device=dev)
+    monkeypatch.setenv("HFG_RB_CONC", "0")
+    monkeypatch.setenv("HFG_RB_SPLIT", rb_split)
+    outs, names = {}, {}
+    for mode in ("0", "1"):
+        monkeypatch.setenv("HFG_FUSE_POST", mode)  # read when the handle is created
+        gen = _gen(pkg, cfg, sd, dev, precision=precision)
+        h = gen.hip_handle(dev)
+        h.profile_reset()
+        h.set_profiling(True)
+        with torch.no_grad():
+            outs[mode] = (gen(mel).cpu().numpy(), gen(mel, lengths=ln).cpu().numpy())
+        torch.cuda.synchronize()
+        h.set_profiling(False)
+        names[mode] = h.profile_summary()
+    assert "conv_post4_tanh" in names["0"] and "conv_post4_tanh" not in names["1"], names["1"]
+    for a, b in zip(outs["0"], outs["1"]):
+        assert np.array_equal(a, b), np.abs(a - b).max()
+    full, rag = outs["1"]
+    assert np.abs(full - _oracle(cfg, sd, mel_np)).max() < ATOL
+    for i, n in enumerate(lens):
+        assert not rag[i, :, C.out_len(cfg, n):].any()
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("precision", ["f16x3", "fp32"])
 def test_conv_post_kernels(pkg, precision):
     """conv_post + tanh: the 4-samples-per-thread kernel where L % 4 == 0 (V1), the

@@ -172,6 +172,8 @@ struct hfg_handle {
                              // layer by layer; the parity suites compare both schedules)
   bool rb_split = true;      // whole-ResBlock split in two launches where it cuts >= 10 % of the
                              // halo recompute (k = 11 in V1; HFG_RB_SPLIT=0: one launch)
+  bool fuse_post = true;     // conv_post + tanh inside the last C = 32 ResBlock launch
+                             // (HFG_FUSE_POST=0: its own kernel; bitwise the same wav)
   int ups_frames = 1;        // k = 2u upsamplers on the output-frame kernel: 1 when its grid
                              // fills the chip, 2 always (HFG_UPS_FRAMES; the polyphase
                              // conv1d_bf16x3 path gives the bitwise same result)
@@ -1105,13 +1107,20 @@ int run_conv(hfg_handle* h, Launcher& ln, const Layer& L, const float* x, int64_
   return HFG_OK;
 }
 
+struct PostFuse {
+  const float* w;  // conv_post weight [C][7], bias [1] (packed fp32)
+  const float* b;
+  float* wav;      // [B][L]
+};
+
 // One whole ResBlock (all dilations) + its MRF contribution in one launch.
 // A split ResBlock (rb.split) runs as two launches through `scratch` (B*C*L floats): convs
 // [0, split) write x after their dilation pairs (MRF-epilogue mode 0: a plain store), convs
 // [split, n) read it back and do the MRF epilogue.  fp32 round trip: bitwise the same x.
+// post: conv_post + tanh fused into the last launch (C = 32, the network's last MRF write).
 int run_resblock(hfg_handle* h, Launcher& ln, const RbFused& rb, const float* x, int64_t B,
                  int64_t Lt, float* mrf, int mrf_mode, float mrf_div, const int32_t* lens,
-                 float* scratch, uint32_t* aout) {
+                 float* scratch, uint32_t* aout, const PostFuse* post = nullptr) {
   const Layer& L0 = h->layers[rb.convs[0]];
   const int C = L0.C_out;
   const int n_all = (int)rb.convs.size();
@@ -1146,8 +1155,18 @@ int run_resblock(hfg_handle* h, Launcher& ln, const RbFused& rb, const float* x,
     p.mrf_rcp = hfg::fast_div_ok(mrf_div) ? 1.0f / mrf_div : 0.0f;
     p.amax_out = last ? aout : nullptr;
     p.dbg = h->dbg_flags;
-    const double bytes =
+    double bytes =
         4.0 * B * Lt * C * ((last && (mrf_mode & 1)) ? 3 : 2) + 4.0 * (double)rb.w_len;
+    if (last && post) {
+      // the stage output is exact on the centre plus conv_post's radius on either side
+      p.halo += 3;
+      p.W = (rb.nwin - 2 * p.halo) & ~3;
+      p.post_w = post->w;
+      p.post_b = post->b;
+      p.wav = post->wav;
+      p.amax_out = nullptr;  // no consumer of the stage output's scale
+      bytes -= 4.0 * B * Lt * (C - 1);
+    }
     const char* name = nullptr;
     ln.begin(flop, bytes);
     hipError_t e =
@@ -1310,10 +1329,12 @@ int run_thin(hfg_handle* h, Launcher& ln, const Stage& st, const float* X, int64
 // f16x3: ax = scale slot of X; aout = slot of out (committed by the write that completes it)
 int run_one_rb(hfg_handle* h, Launcher& ln, const Stage& st, int j, int idx, const float* X,
                int64_t B, int64_t L, float* R, float* Tb, float* out, int mode,
-               const int32_t* lens, const uint32_t* ax, uint32_t* aout) {
+               const int32_t* lens, const uint32_t* ax, uint32_t* aout,
+               const PostFuse* post = nullptr) {
   const hfg_config& c = h->cfg;
   if (st.rbs[j].fused)
-    return run_resblock(h, ln, st.rbs[j], X, B, L, out, mode, (float)c.n_res, lens, Tb, aout);
+    return run_resblock(h, ln, st.rbs[j], X, B, L, out, mode, (float)c.n_res, lens, Tb, aout,
+                        post);
   int rc;
   const uint32_t* asrc = ax;
   for (int m = 0; m < c.n_dil[j]; ++m, ++idx) {
@@ -1369,7 +1390,8 @@ int rb_streams(hfg_handle* h, int part) {
 // ax: f16x3 scale slot of X; aout: slot of out (the MRF mean, or ResBlock only_j's output)
 int run_mrf(hfg_handle* h, Launcher& ln, const Stage& st, const float* X, int64_t B, int64_t L,
             float* R, float* Tb, float* out, const int32_t* lens, int only_j,
-            const uint32_t* ax, uint32_t* aout, const RbConc* conc = nullptr) {
+            const uint32_t* ax, uint32_t* aout, const RbConc* conc = nullptr,
+            const PostFuse* post = nullptr) {
   const hfg_config& c = h->cfg;
   if (st.thin) return run_thin(h, ln, st, X, B, L, out, lens, only_j, aout);
   int rc;
@@ -1418,11 +1440,27 @@ int run_mrf(hfg_handle* h, Launcher& ln, const Stage& st, const float* X, int64_
     const int mode = only_j >= 0 ? 0 : ((j > 0 ? 1 : 0) | (j == c.n_res - 1 ? 2 : 0));
     // the write that completes out: the last ResBlock's (the divide), or only_j's
     rc = run_one_rb(h, ln, st, j, idx, X, B, L, R, Tb, out, mode, lens, ax,
-                    (only_j >= 0 || (mode & 2)) ? aout : nullptr);
+                    (only_j >= 0 || (mode & 2)) ? aout : nullptr,
+                    only_j < 0 && j == c.n_res - 1 ? post : nullptr);
     if (rc) return rc;
     idx += c.n_dil[j];
   }
   return HFG_OK;
+}
+
+// conv_post fused into the last MRF's last ResBlock launch (resblock_bf16x3 conv_post_tail):
+// C = 32 on the one-launch-per-ResBlock schedule, L % 4 == 0, no inspection taps (they read
+// the stage output, which that launch does not store)
+bool post_fusable(const hfg_handle* h, const Stage& st, int64_t L, bool conc_st,
+                  float* const* taps) {
+  const hfg_config& c = h->cfg;
+  if (!h->fuse_post || h->conv_post < 0 || taps || conc_st || st.thin || st.C != 32 ||
+      L % 4 != 0 || h->layers[h->conv_post].C_in != 32)
+    return false;
+  const RbFused& rb = st.rbs[c.n_res - 1];
+  if (!rb.fused || rb.nwin != 512 || rb.wm != 1) return false;
+  const int halo = (rb.split ? rb.halo_p[1] : rb.halo) + 3;
+  return halo >= 4 && ((rb.nwin - 2 * halo) & ~3) >= rb.nwin / 4;
 }
 
 // taps (inspection, hfg_forward_taps): taps[0] <- conv_pre output, taps[1 + 2i] <- ups[i]
@@ -1529,8 +1567,23 @@ int forward_impl(hfg_handle* h, const float* mel, int64_t B, int64_t T, const hf
     if ((rc = tap(1 + 2 * i, X, B * st.C * L))) return rc;
     // MRF (models/hifigan.py:116-131) of ResBlocks (:72-86)
     a_cur = ln.take();
+    const bool conc_st = nb > 4 && stage_conc(h, st, B, L);
+    if (i == c.n_up - 1 && post_fusable(h, st, L, conc_st, taps)) {
+      // the last ResBlock's launch also runs lrelu -> conv_post -> tanh (models/hifigan.py:
+      // 254-256); windows past an item's length write nothing: zero the wav first
+      if (user_lens) {
+        hipError_t e = hipMemsetAsync(wav, 0, sizeof(float) * (size_t)(B * L), stream);
+        if (e != hipSuccess) return hip_fail(e, "hipMemsetAsync(wav)");
+      }
+      const Layer& Lp = h->layers[h->conv_post];
+      const PostFuse pf{h->packed_dev + Lp.w_off, h->packed_dev + Lp.b_off, wav};
+      rc = run_mrf(h, ln, st, X, B, L, R, Tb, MRF, lens_at(i + 1), -1, a_x, a_cur, nullptr, &pf);
+      if (rc) return rc;
+      if (sl.overflow) return fail(HFG_EIO, "internal: f16x3 scale slots exhausted");
+      return HFG_OK;
+    }
     rc = run_mrf(h, ln, st, X, B, L, R, Tb, MRF, lens_at(i + 1), -1, a_x, a_cur,
-                 nb > 4 && stage_conc(h, st, B, L) ? &conc : nullptr);
+                 conc_st ? &conc : nullptr);
     if (rc) return rc;
     if ((rc = tap(2 + 2 * i, MRF, B * st.C * L))) return rc;
     cur = MRF;
@@ -1609,9 +1662,10 @@ int create_impl(const hfg_config* cfg, bool mrf_only, int device, hfg_handle** o
   if (const char* dbg = getenv("HFG_DEBUG_FLAGS")) h->dbg_flags = atoi(dbg);
 #endif
   // schedule choices the parity suites compare (each bitwise invisible, or for the fused
-  // ResBlocks a different rounding order): FUSED_RB, RB_SPLIT, SMALL_TILE, RB_CONC, UPS_FRAMES,
-  // SPLIT
+  // ResBlocks a different rounding order): FUSED_RB, RB_SPLIT, FUSE_POST, SMALL_TILE, RB_CONC,
+  // UPS_FRAMES, SPLIT
   if (const char* fe = getenv("HFG_FUSED_RB")) h->use_fused_rb = atoi(fe) != 0;
+  if (const char* fp = getenv("HFG_FUSE_POST")) h->fuse_post = atoi(fp) != 0;
   if (const char* sp = getenv("HFG_RB_SPLIT")) h->rb_split = atoi(sp) != 0;
   if (const char* st = getenv("HFG_SMALL_TILE")) h->small_tile = atoi(st);
   if (const char* rc = getenv("HFG_RB_CONC")) h->rb_conc = atoi(rc);

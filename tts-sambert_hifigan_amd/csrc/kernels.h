@@ -254,6 +254,12 @@ struct RbParams {
   float mrf_rcp;         // fp32(1 / mrf_div) when fast_div_ok(mrf_div) (exact fma quotient), else 0
   int ew[kRbMaxConv];    // f16x3: packing exponent of each conv's weights (stream order)
   uint32_t* amax_out;    // f16x3: per-item max |stored mrf| slot (final MRF write) or null
+  // fused conv_post + tanh (C = 32, the last MRF write; L % 4 == 0): wav [B][L] written on the
+  // centre [halo, halo + W) of each window, mrf not stored; halo includes the conv's radius 3.
+  // Windows past an item's length write nothing (the host zeroes wav first).  Null: off
+  const float* post_w;   // conv_post weight [C][7] fp32
+  const float* post_b;   // conv_post bias [1]
+  float* wav;
   int dbg;               // ablations (HFG_DEBUG_FLAGS, wrong results when set): bit4 no MRF
                          // epilogue, bit5 no x loads, bit6 no operand writes
 };

@@ -58,6 +58,59 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 typedef float floatx2 __attribute__((ext_vector_type(2)));
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 
+// conv_post + tanh (models/hifigan.py:254-256) fused into the network's last MRF write (C = 32,
+// one 32-row wave per window slice): the exact final x on the window columns [halo - 3,
+// halo + W + 3) is staged as lrelu(x) in LDS ([channel][column + sh] fp32, 0 outside those
+// columns and outside [0, len)), then one thread per 4 consecutive samples sums over
+// (channel, tap) in conv_post4_tanh's order (channel-major, fma from 0, bias last): bitwise the
+// separate kernel's wav, without the stage output's HBM write and read.
+template <int NT, int NWIN, int WN>
+__device__ __forceinline__ void conv_post_tail(const RbParams& p, const floatx16 (&xcur)[1][WN],
+                                               const bool (&ok)[WN], char* lds, int b, int len_b,
+                                               int t0, int tid, int cbase, int half, int col) {
+  constexpr int C = 32, KP = 7;
+  constexpr int S = NWIN + 8;  // row stride (floats): the two lane halves' rows, 4 apart, 32 banks apart
+  typedef float f4 __attribute__((ext_vector_type(4)));
+  float* const s = reinterpret_cast<float*>(lds);
+  const int sh = (4 - (p.halo & 3)) & 3;  // staged column = window column + sh: 16-B aligned quads
+  lds_barrier();                          // every wave is done reading the last conv's operand
+#pragma unroll
+  for (int k = 0; k < WN; ++k)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const float v = xcur[0][k][r];
+      s[((r & 3) + 8 * (r >> 2) + 4 * half) * S + cbase + 32 * k + col + sh] =
+          ok[k] ? (v > 0.f ? v : v * kLReluSlope) : 0.f;
+    }
+  lds_barrier();
+  const float bias = p.post_b[0];
+  float* const wav = p.wav + (int64_t)b * p.L;
+  for (int q = tid; q < p.W / 4; q += NT) {
+    const int t = t0 + 4 * q;  // p.L % 4 == 0 (host): a quad is wholly inside or past the row
+    if (t >= p.L) break;
+    // element k of v = column t - 4 + k (conv_post4_tanh's layout)
+    const float* xs = s + p.halo + sh + 4 * q - 4;
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll 4
+    for (int c = 0; c < C; ++c) {
+      const f4 q0 = *reinterpret_cast<const f4*>(xs + c * S);
+      const f4 q1 = *reinterpret_cast<const f4*>(xs + c * S + 4);
+      const f4 q2 = *reinterpret_cast<const f4*>(xs + c * S + 8);
+      const float v[12] = {q0[0], q0[1], q0[2], q0[3], q1[0], q1[1],
+                           q1[2], q1[3], q2[0], q2[1], q2[2], q2[3]};
+      const float* w = p.post_w + c * KP;
+#pragma unroll
+      for (int o = 0; o < 4; ++o)
+#pragma unroll
+        for (int j = 0; j < KP; ++j) acc[o] = fmaf(w[j], v[o + j + 1], acc[o]);
+    }
+    f4 r;
+#pragma unroll
+    for (int o = 0; o < 4; ++o) r[o] = t + o >= len_b ? 0.f : tanhf(acc[o] + bias);
+    *reinterpret_cast<f4*>(wav + t) = r;
+  }
+}
+
 template <int KT, int WAVES_M, int WAVES_N, int WM, int NP, int FMT>
 __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N, 2)  // 2 waves/SIMD: <= 256 VGPRs
 resblock_bf16x3(const RbParams p) {
@@ -79,6 +132,8 @@ resblock_bf16x3(const RbParams p) {
   constexpr int HPS = 2 * PS;              // half-group (slots 0-7 | 8-15): hi, lo planes
   constexpr int GS = 2 * HPS;              // 16-channel group
   constexpr int ASTEP = 2 * 64 * 16;       // bytes per k-step of one wave row-block (hi, lo)
+  static_assert(C != 32 || (WM == 1 && 32 * (NWIN + 8) * 4 <= NG * GS),
+                "conv_post staging fits the operand planes");
 
   extern __shared__ __attribute__((aligned(16))) char lds[];
   float* const bias_s = reinterpret_cast<float*>(lds + NG * GS);
@@ -470,12 +525,16 @@ resblock_bf16x3(const RbParams p) {
       (void*)(p.mrf + (int64_t)b * p.bs), 0, (int)0xFFFFFFFFu, 0x00020000);
   const bool add = p.mrf_mode & 1;
   const bool div = p.mrf_mode & 2;
+  // fused conv_post (C = 32, the network's last MRF write): the stage output is not stored;
+  // it is computed on the centre plus the conv's radius 3 on either side and consumed from LDS
+  const bool post = C == 32 && p.wav != nullptr;
+  const int c_lo = post ? p.halo - 3 : p.halo, c_hi = post ? p.halo + p.W + 3 : p.halo + p.W;
   bool ok[WN];
   unsigned vo[WN];
 #pragma unroll
   for (int k = 0; k < WN; ++k) {
     const int c = cbase + 32 * k + col;
-    ok[k] = vk[k] && c >= p.halo && c < p.halo + p.W;
+    ok[k] = vk[k] && c >= c_lo && c < c_hi;
     vo[k] = ok[k] ? (lrow + (unsigned)(ws + c)) * 4u : 0u;
   }
   // every MRF load is issued before any use (one wait for all 16 x WN), then the adds /
@@ -523,9 +582,12 @@ resblock_bf16x3(const RbParams p) {
     for (int k = 0; k < WN; ++k)
 #pragma unroll
       for (int r = 0; r < 16; ++r) asm volatile("" ::"v"(xcur[i][k][r]));
+  if constexpr (C == 32) {
+    if (post) conv_post_tail<NT, NWIN, WN>(p, xcur, ok, lds, b, len_b, t0, tid, cbase, half, col);
+  }
 #pragma unroll
   for (int k = 0; k < WN; ++k) {
-    if (ok[k]) {
+    if (ok[k] && !post) {
 #pragma unroll
       for (int i = 0; i < WM; ++i)
 #pragma unroll
@@ -614,6 +676,9 @@ hipError_t launch_resblock_bf16x3(int C, int nwin, int wm, int kt, int fmt, int 
   if (p.n_conv < 2 || p.n_conv > kRbMaxConv || (p.n_conv & 1)) return hipErrorInvalidValue;
   if (p.conv0 < 0 || p.conv0 + p.n_conv > p.n_conv_stream) return hipErrorInvalidValue;
   if (p.W <= 0 || p.halo < 0 || p.W + 2 * p.halo > nwin) return hipErrorInvalidValue;
+  if (p.wav && (C != 32 || wm != 1 || p.L % 4 || p.W % 4 || p.halo < 4 || !p.post_w || !p.post_b ||
+                p.amax_out))
+    return hipErrorInvalidValue;
   for (int i = 0; i < p.n_conv; ++i)
     if (p.dil[i] < 1 || (kt - 1) / 2 * p.dil[i] > rb_marg(C, nwin)) return hipErrorInvalidValue;
   {
