@@ -139,3 +139,29 @@ def test_default_precision_from_environment(pkg, monkeypatch):
     monkeypatch.setenv("HFG_PRECISION", "fp16")
     with pytest.raises(ValueError):
         pkg.HiFiGANGenerator(**C.V2STAR.kwargs())
+
+
+def test_weight_cache_tracks_replaced_parameters_without_global_hook(pkg):
+    """The module caches its (key, tensor) list and re-checks, per forward, that every cached
+    tensor is still the one its conv holds: replacing a parameter or applying / removing
+    weight norm rebuilds it.  Importing the package installs no process-wide
+    nn.Module parameter-registration hook."""
+    import torch.nn.modules.module as M
+    assert not M._global_parameter_registration_hooks
+    gen = pkg.HiFiGANGenerator(**C.V2STAR.kwargs())
+    items = dict(gen._items())
+    assert list(items) == list(gen.state_dict())
+    new_w = torch.nn.Parameter(torch.zeros_like(gen.ups[1].weight))
+    gen.ups[1].weight = new_w
+    assert dict(gen._items())["ups.1.weight"] is new_w
+    gen.apply_weight_norm()
+    keys = [k for k, _ in gen._items()]
+    assert "ups.0.weight_g" in keys and "ups.0.weight" not in keys
+    assert sorted(keys) == sorted(gen.state_dict())
+    gen.remove_weight_norm()
+    assert sorted(k for k, _ in gen._items()) == sorted(gen.state_dict())
+    rb = gen.mrfs[0].resblocks[1]
+    rb._items()
+    b = torch.nn.Parameter(torch.ones_like(rb.convs2[0].bias))
+    rb.convs2[0].bias = b
+    assert dict(rb._items())["resblocks.0.convs2.0.bias"] is b

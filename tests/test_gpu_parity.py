@@ -208,7 +208,9 @@ def test_split_layer_kernels_run_to_run_bitwise(pkg, precision, fused, monkeypat
     whole-ResBlock kernel off the 64x256 / 32x256 tiles run every C <= 64 conv).  Guards
     the per-wave vmcnt count of the staged input window (a wait that let a chunk read a
     weight slab before its DMA landed gave nondeterministic errors up to ~6e-4, round 1) and,
-    for f16x3, the order-free max of the per-item scale slots."""
+    for f16x3, the order-free max of the per-item scale slots and the exclusion of stale LDS
+    margin rows from the block maxima: forwards of other configurations (x4 weights, loud
+    mels) run between the repeats."""
     from oracle import config as C, prng
     monkeypatch.setenv("HFG_FUSED_RB", fused)
     dev = _dev()
@@ -218,12 +220,22 @@ def test_split_layer_kernels_run_to_run_bitwise(pkg, precision, fused, monkeypat
     mel = torch.as_tensor(prng.mel_input(23, (B, cfg.n_mels, T))).to(dev)
     lens = torch.tensor([1000, 731, 1000, 2, 517], dtype=torch.int32, device=dev)
     gen = _gen(pkg, cfg, sd, dev, precision=precision)
+    # forwards of other configurations between the repeats leave other values in LDS, in
+    # the per-item scale slots and in the cached workspace
+    dirt = []
+    for preset, seed in (("v2star", 61), ("nonexact", 62)):
+        ocfg = C.PRESETS[preset]
+        osd = {k: v * 4.0 for k, v in C.make_state_dict(ocfg, seed=seed).items()}
+        dirt.append((_gen(pkg, ocfg, osd, dev, precision=precision),
+                     torch.as_tensor(30.0 * prng.mel_input(seed, (3, ocfg.n_mels, 333))).to(dev)))
     h = gen.hip_handle(dev)
     outs = []
-    for n in (1, 2, 1, 2, 1, 2):
+    for i, n in enumerate((1, 2, 1, 2, 1, 2)):
         h.set_streams(n)
         with torch.no_grad():
             outs.append((gen(mel).cpu().numpy(), gen(mel, lengths=lens).cpu().numpy()))
+            og, om = dirt[i % 2]
+            og(om)
         torch.cuda.synchronize()
     h.set_streams(2)
     for o in outs[1:]:

@@ -13,6 +13,12 @@ import numpy as np
 import pytest
 import torch
 
+
+
+def _randn(*shape, seed, dev):
+    """Seeded device input (every GPU test input is reproducible from the record)."""
+    return torch.randn(*shape, generator=torch.Generator().manual_seed(seed)).to(dev)
+
 pytestmark = pytest.mark.gpu
 ATOL = 1e-4
 
@@ -43,7 +49,7 @@ def run(gen, mel):
 # ---- reference contract (tests/test_hifigan_generator.py) -------------------------
 def test_forward_shape_and_range(v1, dev):
     gen, _ = v1
-    mel = torch.randn(2, 80, 100, device=dev)
+    mel = _randn(2, 80, 100, seed=301, dev=dev)
     wav = run(gen, mel)
     assert wav.shape == (2, 1, 100 * 256)
     assert wav.dtype == torch.float32
@@ -52,13 +58,13 @@ def test_forward_shape_and_range(v1, dev):
 
 @pytest.mark.parametrize("T", [50, 100, 200])
 def test_different_lengths(v1, dev, T):
-    wav = run(v1[0], torch.randn(1, 80, T, device=dev))
+    wav = run(v1[0], _randn(1, 80, T, seed=302, dev=dev))
     assert wav.shape == (1, 1, T * 256)
 
 
 @pytest.mark.parametrize("B", [1, 4, 8])
 def test_batch_sizes(v1, dev, B):
-    wav = run(v1[0], torch.randn(B, 80, 100, device=dev))
+    wav = run(v1[0], _randn(B, 80, 100, seed=303, dev=dev))
     assert wav.shape == (B, 1, 100 * 256)
 
 
@@ -66,13 +72,13 @@ def test_nonexact_upsampling_shape(pkg, dev):
     # reference test_hifigan_integration.py:147-164; oracle gives [1, 1, 10048] for T=50
     gen = pkg.HiFiGAN(n_mels=80, upsample_rates=[5, 5, 4, 2],
                       upsample_kernel_sizes=[10, 10, 8, 4]).to(dev).eval()
-    wav = run(gen, torch.randn(1, 80, 50, device=dev))
+    wav = run(gen, _randn(1, 80, 50, seed=304, dev=dev))
     assert wav.shape == (1, 1, 10048)
 
 
 def test_generate_alias_and_logging(pkg, dev):
     model = pkg.HiFiGAN(n_mels=80, debug_shapes=True).to(dev).eval()
-    mel = torch.randn(1, 80, 10, device=dev)
+    mel = _randn(1, 80, 10, seed=305, dev=dev)
     buf = io.StringIO()
     old, sys.stdout = sys.stdout, buf
     try:
@@ -91,7 +97,7 @@ def test_inputs_rejected(v1, dev):
     with pytest.raises(RuntimeError):
         gen(torch.randn(1, 80, 8))  # CPU tensor: no CPU fallback
     with pytest.raises(RuntimeError):
-        gen(torch.randn(1, 81, 8, device=dev))
+        gen(_randn(1, 81, 8, seed=306, dev=dev))
     mel = torch.randn(1, 80, 8, device=dev, requires_grad=True)
     with pytest.raises(NotImplementedError):
         gen(mel)
@@ -177,7 +183,7 @@ def test_profiling_summary(pkg, v1, dev):
     h = gen.hip_handle(dev)
     h.profile_reset()
     h.set_profiling(True)
-    run(gen, torch.randn(1, 80, 64, device=dev))
+    run(gen, _randn(1, 80, 64, seed=307, dev=dev))
     h.set_profiling(False)
     prof = h.profile_summary()
     # the default (f16x3) schedule: conv_pre, 4 upsamplers, conv_post, the stage-0 and stage-1
@@ -202,7 +208,7 @@ def test_hipgraph_capture_replay(v1, dev):
     """The 78 launches of one forward can be captured into a hipGraph (torch.cuda.graph
     on the capture stream) and replayed; the replay equals the eager result."""
     gen, _ = v1
-    mel = torch.randn(2, 80, 40, device=dev)
+    mel = _randn(2, 80, 40, seed=308, dev=dev)
     with torch.no_grad():
         ref = gen(mel)
         s = torch.cuda.Stream(dev)
@@ -213,7 +219,7 @@ def test_hipgraph_capture_replay(v1, dev):
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
             out = gen(mel)
-        mel.copy_(torch.randn(2, 80, 40, device=dev))
+        mel.copy_(_randn(2, 80, 40, seed=309, dev=dev))
         g.replay()
         ref2 = gen(mel)
     torch.cuda.synchronize()
@@ -336,7 +342,7 @@ def test_weight_edit_through_data_is_picked_up(pkg, dev):
     ref = H.generator_forward(sd2, cfg, mel.cpu())
     assert (w1.cpu() - ref).abs().max().item() < ATOL
     rb = gen.mrfs[0].resblocks[1]
-    x = torch.randn(2, rb.channels, 50, device=dev)
+    x = _randn(2, rb.channels, 50, seed=310, dev=dev)
     y0 = run(rb, x).clone()
     rb.convs1[0].weight.data.neg_()
     assert not torch.equal(y0, run(rb, x))
@@ -355,7 +361,7 @@ def test_hipgraph_capture_two_stream_forward(v1, dev):
     gen, _ = v1
     h = gen.hip_handle(dev)
     h.set_streams(2)
-    mel = torch.randn(4, 80, 1100, device=dev)
+    mel = _randn(4, 80, 1100, seed=311, dev=dev)
     with torch.no_grad():
         s = torch.cuda.Stream(dev)
         s.wait_stream(torch.cuda.current_stream(dev))
@@ -365,7 +371,7 @@ def test_hipgraph_capture_two_stream_forward(v1, dev):
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
             out = gen(mel)
-        mel.copy_(torch.randn(4, 80, 1100, device=dev))
+        mel.copy_(_randn(4, 80, 1100, seed=312, dev=dev))
         g.replay()
         torch.cuda.synchronize()
         ref = gen(mel)

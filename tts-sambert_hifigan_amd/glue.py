@@ -49,10 +49,15 @@ class StreamingVocoder:
 
     A chunk of ``chunk_frames`` new frames is emitted once ``context`` future frames
     exist; it is computed from the frames ``[start - context, end + context)`` and
-    cropped, so the concatenated audio of a stream is BITWISE the one-shot
-    ``gen(full_mel)`` (``context`` defaults to ``gen.receptive_field_frames()``, beyond
-    which an output sample does not depend on the input: no overlap-add or crossfade is
-    needed, the seams are exact).  Needs an exact-upsampling config (out = T x hop).
+    cropped (``context`` defaults to ``gen.receptive_field_frames()``, beyond which an
+    output sample does not depend on the input: no overlap-add or crossfade is needed).
+    Every chunk is bitwise the crop of ``gen(window)``.  In the exact-arithmetic modes
+    (fp32, bf16x3) the concatenated stream is therefore BITWISE the one-shot
+    ``gen(full_mel)``; in f16x3 each launch scales its operands by a power of two from
+    the max over the item it sees — the window here, the whole utterance one-shot — and
+    values whose f16 lo half falls below the normal range (< 2^-17 of that max) round on a
+    different grid, so the stream equals the one-shot run to ~1e-8 (tested <= 1e-7) and
+    the reference to the same 1e-4.  Needs an exact-upsampling config (out = T x hop).
 
     Bounded state: a stream keeps only the frames ``[emitted - context, received)``.  Each
     stream owns one fixed buffer whose live columns start at a moving offset: a step only
@@ -94,6 +99,7 @@ class StreamingVocoder:
         self._emitted = [0] * self.n_streams   # frames whose audio was returned
         self.chunks_run = 0
         self.compactions = 0
+        self.last_windows: Dict[int, tuple] = {}  # stream -> (a, b, lo, hi) of the last step
 
     # -- state -------------------------------------------------------------------------
     @property
@@ -186,6 +192,7 @@ class StreamingVocoder:
         with torch.no_grad():
             wav = self.gen(mel, lengths=None if min(lens) == W else lens)
         out = {}
+        self.last_windows = {s: w for s, w in ready}
         for i, (s, (a, b, lo, hi)) in enumerate(ready):
             out[s] = wav[i, 0, (a - lo) * self.hop:(b - lo) * self.hop]
             if self.debug_shapes:

@@ -25,27 +25,12 @@ autograd; a CPU input or an input that requires grad raises.
 from __future__ import annotations
 
 import os
-import weakref
 from typing import Dict, List, Optional, Tuple
 
 import torch
 import torch.nn as nn
 
 from . import _lib
-
-
-def _on_param_registered(module, name, param):
-    """Global nn.Module parameter-registration hook: a conv owned by a HIP module got a
-    new parameter object (replacement, weight norm applied / removed) -> its owners
-    re-read their parameter list and re-pack before the next forward."""
-    owners = module.__dict__.get("_hfg_owners")
-    if owners:
-        for o in list(owners):
-            o.refresh_weights()
-    return None
-
-
-nn.modules.module.register_module_parameter_registration_hook(_on_param_registered)
 
 
 def _lengths_on(lengths, device) -> torch.Tensor:
@@ -103,6 +88,7 @@ class _HipWeights(nn.Module):
         self._hfg_fingerprint: Dict[int, tuple] = {}
         self._hfg_checksum: Dict[int, torch.Tensor] = {}
         self._hfg_items = None  # cached (key, tensor) list, rebuilt after any invalidation
+        self._hfg_slots = []    # (conv, parameter name, tensor) the cache was built from
         self.precision = precision
         self.register_load_state_dict_post_hook(_HipWeights._after_load)
 
@@ -120,34 +106,36 @@ class _HipWeights(nn.Module):
 
     def _apply(self, fn, *args, **kwargs):
         out = super()._apply(fn, *args, **kwargs)
-        # parameters moved / converted (possibly of a submodule shared with another owner)
-        for m in self.modules():
-            for o in list(getattr(m, "_hfg_owners", ())):
-                o.refresh_weights()
-        self.refresh_weights()
+        self.refresh_weights()  # a shared submodule moved elsewhere shows in data_ptr
         return out
 
     def _items(self):
         """The (key, tensor) list, cached: walking the module tree costs ~0.6 ms for V1,
-        more than a C1 forward's host budget.  A parameter (re)registered on any conv of
-        this module (``conv.weight = Parameter(..)``, weight norm applied / removed) fires
-        the registration hook below, which drops the cache."""
+        more than a C1 forward's host budget.  Every forward checks that each cached tensor
+        is still the one its conv holds (one dict lookup per parameter, ~15 us for V1), so a
+        parameter replaced on any conv (``conv.weight = Parameter(..)``, weight norm applied
+        or removed) rebuilds the list — no process-wide hook is installed."""
         items = self._hfg_items
+        if items is not None and any(m._parameters.get(p) is not t
+                                     for m, p, t in self._hfg_slots):
+            items = None
         if items is None:
-            items = list(self._hip_weight_items())
-            for m in self.modules():
-                if isinstance(m, (nn.Conv1d, nn.ConvTranspose1d)):
-                    owners = m.__dict__.get("_hfg_owners")
-                    if owners is None:
-                        owners = weakref.WeakSet()
-                        m.__dict__["_hfg_owners"] = owners
-                    owners.add(self)
-            self._hfg_items = items
+            items, slots = [], []
+            for key, mod, p in self._hip_weight_slots():
+                t = getattr(mod, p)
+                items.append((key, t))
+                if p in mod._parameters:
+                    slots.append((mod, p, t))
+            self._hfg_items, self._hfg_slots = items, slots
         return items
 
-    # subclasses: (key, tensor) of every parameter in the handle's key space, and the handle
-    def _hip_weight_items(self):
+    # subclasses: (key, module, parameter name) of every parameter in the handle's key
+    # space, and the handle
+    def _hip_weight_slots(self):
         raise NotImplementedError
+
+    def _hip_weight_items(self):
+        return [(key, getattr(mod, p)) for key, mod, p in self._hip_weight_slots()]
 
     def _hip_new_handle(self, idx: int) -> _lib.Handle:
         raise NotImplementedError
@@ -181,16 +169,14 @@ class _HipWeights(nn.Module):
         return h
 
     @staticmethod
-    def _conv_items(module: nn.Module, prefix: str = ""):
+    def _conv_slots(module: nn.Module, prefix: str = ""):
         for name, mod in module.named_modules():
             if not isinstance(mod, (nn.Conv1d, nn.ConvTranspose1d)):
                 continue
-            if hasattr(mod, "weight_g") and hasattr(mod, "weight_v"):
-                yield prefix + name + ".weight_g", mod.weight_g
-                yield prefix + name + ".weight_v", mod.weight_v
-            else:
-                yield prefix + name + ".weight", mod.weight
-            yield prefix + name + ".bias", mod.bias
+            names = (("weight_g", "weight_v") if hasattr(mod, "weight_g") and hasattr(mod, "weight_v")
+                     else ("weight",))
+            for p in names + ("bias",):
+                yield prefix + name + "." + p, mod, p
 
     def _run_block(self, x: torch.Tensor, channels: int, resblock: int) -> torch.Tensor:
         """y = MRF(x) (resblock < 0) or ResBlock_resblock(x) on the HIP device."""
@@ -236,8 +222,8 @@ class ResBlock(_HipWeights):
                                          padding=get_padding(kernel_size, 1)))
         self._hip_setup(precision)
 
-    def _hip_weight_items(self):
-        return self._conv_items(self, "resblocks.0.")
+    def _hip_weight_slots(self):
+        return self._conv_slots(self, "resblocks.0.")
 
     def _hip_new_handle(self, idx):
         cfg = _lib.make_mrf_config(self.channels, [self.kernel_size], [list(self.dilation)],
@@ -270,8 +256,8 @@ class MRF(_HipWeights):
                                            precision=precision))
         self._hip_setup(precision)
 
-    def _hip_weight_items(self):
-        return self._conv_items(self)
+    def _hip_weight_slots(self):
+        return self._conv_slots(self)
 
     def _hip_new_handle(self, idx):
         cfg = _lib.make_mrf_config(self.channels, self.resblock_kernel_sizes,
@@ -328,9 +314,10 @@ class HiFiGANGenerator(_HipWeights):
         self.set_precision(self.precision)
 
     def set_precision(self, precision: str):
-        """"fp32" (exact fp32 MFMA, default), "bf16x3" (fp32 operands split into
-        two bf16 halves on the bf16 matrix cores; within ~1e-5 of the reference at
-        default weight scale) or "bf16w" (conv weights stored as bf16 — rounded when
+        """"f16x3" (the module default, ``default_precision``: fp32 operands scaled by a
+        power of two and split into two f16 halves on the f16 matrix cores, fp32-class
+        products), "fp32" (exact fp32 MFMA; the C ABI's zero-initialised default),
+        "bf16x3" (two bf16 halves; within ~1e-5 of the reference at default weight scale) or "bf16w" (conv weights stored as bf16 — rounded when
         committed to the handle, the module's own parameters untouched — activations
         still split: the reference model with bf16-cast weights, to 1e-4).  Applies to
         the MRF / ResBlock submodules too."""
@@ -343,12 +330,13 @@ class HiFiGANGenerator(_HipWeights):
         return self
 
     # ------------------------------------------------------------------
-    def _hip_weight_items(self):
-        """(state_dict-style key, tensor) of every parameter the kernels need,
+    def _hip_weight_slots(self):
+        """(state_dict-style key, conv, name) of every parameter the kernels need,
         with weight_g / weight_v passed through for weight-normed modules."""
-        return self._conv_items(self)
+        return self._conv_slots(self)
 
-    _weight_tensors = _hip_weight_items
+    def _weight_tensors(self):
+        return self._hip_weight_items()
 
     def _hip_new_handle(self, idx):
         return _lib.Handle(self._hfg_cfg, idx)
