@@ -19,12 +19,16 @@ extern "C" {
 #endif
 
 /* Copy the packed image of one layer (module prefix, e.g. "ups.0") into out:
- * w_len packed GEMM weights followed by b_len per-row biases.  info[11]
+ * w_len packed GEMM weights followed by b_len per-row biases.  info[10]
  * receives {kind (0 conv, 1 ups, 2 post), M, KT, tile, m_tiles, n_chunks,
- * w_len, b_len, CK, MT, ew} (ew: the f16x3 packing exponent — the split planes hold
- * f16 halves of w * 2^ew; 0 otherwise).  With out == NULL only info is filled. */
+ * w_len, b_len, CK, MT}.  With out == NULL only info is filled (no commit). */
 int hfg_debug_packed_layer(hfg_handle* h, const char* mod, float* out, size_t cap,
                            int64_t* info);
+
+/* *ew <- the f16x3 packing exponent of layer `mod` (its split planes hold f16 halves of
+ * w * 2^ew; 0 in the other modes).  Commits pending weights first and returns that
+ * commit's error (HFG_EINVAL while a weight is missing). */
+int hfg_debug_layer_exponent(hfg_handle* h, const char* mod, int* ew);
 
 /* Packed image of the whole-ResBlock launch of stage `stage`, ResBlock `j`
  * (resblock_bf16x3.hip; split-precision handles, stages with 32, 64 or 128 channels):

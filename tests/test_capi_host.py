@@ -31,7 +31,7 @@ def header_symbols():
 def test_library_exports_every_header_symbol(pkg):
     lib = pkg.load_library()
     syms = header_symbols()
-    assert len(syms) == 39
+    assert len(syms) == 40
     for s in sorted(syms):
         assert hasattr(lib, s), f"missing export {s}"
     assert set(syms) == set(pkg._lib.SIGNATURES), "ctypes signatures out of sync with headers"
@@ -498,3 +498,41 @@ def test_bf16w_packing(pkg, preset):
             ref = _bf16_rne(W).ravel()
             assert np.array_equal(nz, np.sort(ref[ref != 0])), mod
     assert n_split >= 3 and n_fp32 >= 1
+
+
+def test_layer_exponent_entry_commits_or_reports(pkg):
+    """hfg_debug_layer_exponent: with a weight missing it returns the commit's
+    error instead of a stale 0; info-only hfg_debug_packed_layer fills exactly 10 entries and
+    does not commit."""
+    import ctypes
+    cfg = C.V2STAR
+    h = host_handle(pkg, cfg, precision="f16x3")
+    lib = pkg.load_library()
+    sd = C.make_state_dict(cfg, seed=6)
+    keys = list(sd)
+    for k in keys[:-1]:
+        h.set_weight(k, torch.from_numpy(sd[k]))
+    ew = ctypes.c_int(-99)
+    assert lib.hfg_debug_layer_exponent(h.ptr, b"ups.1", ctypes.byref(ew)) != 0
+    assert ew.value == -99
+    info = (ctypes.c_int64 * 11)(*([-7] * 11))
+    assert lib.hfg_debug_packed_layer(h.ptr, b"ups.1", None, 0, info) == 0
+    assert info[10] == -7 and info[9] > 0
+    h.set_weight(keys[-1], torch.from_numpy(sd[keys[-1]]))
+    assert lib.hfg_debug_layer_exponent(h.ptr, b"ups.1", ctypes.byref(ew)) == 0
+    w = sd["ups.1.weight"]
+    assert ew.value == 15 - int(np.frexp(np.abs(w).max())[1])
+
+
+def test_removed_knob_value_is_refused(pkg, monkeypatch):
+    """HFG_UPS_FRAMES=0 (the polyphase-only schedule, removed in round 4) is refused at create
+    instead of silently running the default schedule."""
+    lib = pkg.load_library()
+    c = pkg.make_config(80, [8, 8, 2, 2], [16, 16, 4, 4], 512, [3, 7, 11], [[1, 3, 5]] * 3)
+    monkeypatch.setenv("HFG_UPS_FRAMES", "0")
+    h = ctypes.c_void_p()
+    assert lib.hfg_create(ctypes.byref(c), -1, ctypes.byref(h)) == -22
+    assert b"HFG_UPS_FRAMES" in lib.hfg_last_error()
+    monkeypatch.setenv("HFG_UPS_FRAMES", "2")
+    assert lib.hfg_create(ctypes.byref(c), -1, ctypes.byref(h)) == 0
+    lib.hfg_destroy(h)

@@ -161,6 +161,7 @@ SIGNATURES = {
     "hfg_profile_summary": (c_int, [c_void_p, c_char_p, c_size_t]),
     "hfg_debug_packed_layer": (c_int, [c_void_p, c_char_p, POINTER(c_float), c_size_t,
                                        POINTER(c_int64)]),
+    "hfg_debug_layer_exponent": (c_int, [c_void_p, c_char_p, POINTER(c_int)]),
     "hfg_debug_packed_resblock": (c_int, [c_void_p, c_int, c_int, POINTER(c_float), c_size_t,
                                           POINTER(c_int64)]),
     "hfg_mrf_create": (c_int, [POINTER(HfgMrfConfig), c_int, POINTER(c_void_p)]),
@@ -359,14 +360,18 @@ class Handle:
     def packed_layer(self, mod: str):
         """(info dict, packed weights np.ndarray, per-row bias np.ndarray) of one layer."""
         import numpy as np
-        info = (c_int64 * 11)()
+        info = (c_int64 * 10)()
         check(self.lib.hfg_debug_packed_layer(self.ptr, mod.encode(), None, 0, info))
         w_len, b_len = int(info[6]), int(info[7])
         out = np.zeros(w_len + b_len, dtype=np.float32)
         check(self.lib.hfg_debug_packed_layer(
             self.ptr, mod.encode(), out.ctypes.data_as(POINTER(c_float)), out.size, info))
-        keys = ["kind", "M", "KT", "tile", "m_tiles", "n_chunks", "w_len", "b_len", "CK", "MT", "ew"]
-        return dict(zip(keys, [int(v) for v in info])), out[:w_len], out[w_len:]
+        ew = c_int(0)
+        check(self.lib.hfg_debug_layer_exponent(self.ptr, mod.encode(), ctypes.byref(ew)))
+        keys = ["kind", "M", "KT", "tile", "m_tiles", "n_chunks", "w_len", "b_len", "CK", "MT"]
+        d = dict(zip(keys, [int(v) for v in info]))
+        d["ew"] = int(ew.value)
+        return d, out[:w_len], out[w_len:]
 
     def packed_resblock(self, stage: int, j: int):
         """(info dict, packed A stream, biases) of a whole-ResBlock launch, or

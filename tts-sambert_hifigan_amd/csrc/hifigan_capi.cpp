@@ -182,6 +182,9 @@ struct hfg_handle {
   int small_tile = -1;       // small-grid tile: -1 auto (grid < kSmallGridBlocks), 0 never,
                              // 1 always (HFG_SMALL_TILE; bitwise invisible)
   int dbg_flags = 0;  // HFG_DEBUG_FLAGS (kernel ablations, -DHFG_ABLATE=1 builds only)
+  // HFG_STAGGER="conv,rb": microseconds the first round's second-half blocks in the
+  // multi-round tile-5 layer-conv and whole-ResBlock grids wait (experiment; 0 = off)
+  int stag_conv = 0, stag_rb = 0;
   // batch split over two HIP streams (HFG_SPLIT=1 disables): the two halves' launches
   // overlap, so one half's ramp-down / epilogue tail runs beside the other's main loops
   int split = 2;
@@ -460,7 +463,13 @@ int build_layers(hfg_handle* h) {
         std::vector<int> hd;  // receptive-field radius of each dilation pair
         for (int m = 0; m < c.n_dil[j]; ++m)
           hd.push_back((rb.kt - 1) / 2 * c.dil[j][m] + (rb.kt - 1) / 2);
-        const double whole = (double)nwin / rb.W;
+        // the network's last MRF write may carry the fused conv_post (post_fusable): its
+        // launch (the last part) is exact on conv_post's radius 3 more on either side
+        const int post = h->fuse_post && i + 1 == h->stages.size() && j == c.n_res - 1 &&
+                                 C == 32 && h->conv_post >= 0
+                             ? 3 : 0;
+        const int w_whole = (nwin - 2 * (rb.halo + post)) & ~3;
+        const double whole = w_whole >= nwin / 4 ? (double)nwin / w_whole : 1e9;
         double best = whole;
         for (int m = 1; m < c.n_dil[j]; ++m) {
           int h0 = 0, h1 = 0;
@@ -469,8 +478,9 @@ int build_layers(hfg_handle* h) {
           h0 -= (rb.kt - 1) / 2 * c.dil[j][0];  // each part's first conv: exact (margins)
           h1 -= (rb.kt - 1) / 2 * c.dil[j][m];
           const int w0 = (nwin - 2 * h0) & ~3, w1 = (nwin - 2 * h1) & ~3;
-          if (w0 < nwin / 4 || w1 < nwin / 4) continue;
-          const double cost = ((double)m * nwin / w0 + (double)(c.n_dil[j] - m) * nwin / w1) /
+          const int w1p = (nwin - 2 * (h1 + post)) & ~3;  // the launch as it runs
+          if (w0 < nwin / 4 || w1p < nwin / 4) continue;
+          const double cost = ((double)m * nwin / w0 + (double)(c.n_dil[j] - m) * nwin / w1p) /
                               c.n_dil[j];
           if (cost < best) {
             best = cost;
@@ -1091,6 +1101,11 @@ int run_conv(hfg_handle* h, Launcher& ln, const Layer& L, const float* x, int64_
   const int ntile = L.prec == 1 ? hfg::kBf16x3Tiles[L.tile].NTILE() : kTiles[L.tile].NTILE();
   int n_tiles = (int)((Lt + ntile - 1) / ntile), m_tiles = L.m_tiles;
   const int tile = pick_tile(h, L, p, Lt, B, ln.conc, n_tiles, m_tiles);
+  if (h->stag_conv > 0 && hfg::kBf16x3Tiles[tile].AREG && (int64_t)n_tiles * m_tiles * B >= 1024) {
+    p.stag_lo = 256;
+    p.stag_hi = 512;
+    p.stag_n = h->stag_conv;
+  }
   const double flop = 2.0 * L.C_out * L.C_in * L.k * (double)Lt * B;
   double bytes = 4.0 * B * Lt * (L.C_in + L.C_out) + 4.0 * L.C_out * L.C_in * L.k;
   if (res) bytes += 4.0 * B * Lt * L.C_out;
@@ -1155,6 +1170,16 @@ int run_resblock(hfg_handle* h, Launcher& ln, const RbFused& rb, const float* x,
     p.mrf_rcp = hfg::fast_div_ok(mrf_div) ? 1.0f / mrf_div : 0.0f;
     p.amax_out = last ? aout : nullptr;
     p.dbg = h->dbg_flags;
+    if (h->stag_rb > 0) {
+      // resident blocks per CU from the LDS footprint (256 CUs)
+      const int per_cu = hfg::rb_lds_bytes(C, rb.nwin, n_all) <= 80 * 1024 ? 2 : 1;
+      const int64_t blocks = (Lt + p.W - 1) / p.W * B;
+      if (blocks >= 2 * 256 * per_cu) {
+        p.stag_lo = 128 * per_cu;
+        p.stag_hi = 256 * per_cu;
+        p.stag_n = h->stag_rb;
+      }
+    }
     double bytes =
         4.0 * B * Lt * C * ((last && (mrf_mode & 1)) ? 3 : 2) + 4.0 * (double)rb.w_len;
     if (last && post) {
@@ -1661,6 +1686,24 @@ int create_impl(const hfg_config* cfg, bool mrf_only, int device, hfg_handle** o
 #if HFG_ABLATE
   if (const char* dbg = getenv("HFG_DEBUG_FLAGS")) h->dbg_flags = atoi(dbg);
 #endif
+  if (const char* sg = getenv("HFG_STAGGER")) sscanf(sg, "%d,%d", &h->stag_conv, &h->stag_rb);
+  // knobs of earlier rounds' schedules that no longer exist: say so instead of silently
+  // running the default schedule under a variant's label
+  {
+    static const char* const removed[] = {
+        "HFG_SPLIT_MIN", "HFG_SPLIT_LAG", "HFG_SPLIT_STAGGER", "HFG_RB_NCH", "HFG_RB_NCH_BLOCKS",
+        "HFG_UPS_SMALL_ROWS", "HFG_RB_WMR", "HFG_RB_WM", "HFG_RB_SPLIT_MIN", "HFG_RB_SPLIT_TH",
+        "HFG_RB64_NARROW", "HFG_MFMA16", "HFG_EPI_LDS", "HFG_AREG", "HFG_UPS_SWIZZLE",
+        "HFG_UPS_PLANES", "HFG_UPS_NT", "HFG_UPS_NT2", "HFG_THIN_MFMA", "HFG_POST4",
+        "HFG_SMALL_GRID", "HFG_RB_WN32", "HFG_C16", "HFG_BF16X3_BIGTILE"};
+    static std::once_flag warned;
+    std::call_once(warned, [] {
+      for (const char* k : removed)
+        if (getenv(k))
+          fprintf(stderr, "[hifigan_hip] %s is set but no longer read (a removed schedule knob); "
+                          "the default schedule runs\n", k);
+    });
+  }
   // schedule choices the parity suites compare (each bitwise invisible, or for the fused
   // ResBlocks a different rounding order): FUSED_RB, RB_SPLIT, FUSE_POST, SMALL_TILE, RB_CONC,
   // UPS_FRAMES, SPLIT
@@ -1669,7 +1712,16 @@ int create_impl(const hfg_config* cfg, bool mrf_only, int device, hfg_handle** o
   if (const char* sp = getenv("HFG_RB_SPLIT")) h->rb_split = atoi(sp) != 0;
   if (const char* st = getenv("HFG_SMALL_TILE")) h->small_tile = atoi(st);
   if (const char* rc = getenv("HFG_RB_CONC")) h->rb_conc = atoi(rc);
-  if (const char* uf = getenv("HFG_UPS_FRAMES")) h->ups_frames = atoi(uf) == 2 ? 2 : 1;
+  if (const char* uf = getenv("HFG_UPS_FRAMES")) {
+    // 0 (never the output-frame upsampler) was removed in round 4
+    const int v = atoi(uf);
+    if (v != 1 && v != 2) {
+      delete h;
+      return fail(HFG_EINVAL, "HFG_UPS_FRAMES=%s: expected 1 (default) or 2 (force the "
+                              "output-frame upsampler); 0 was removed", uf);
+    }
+    h->ups_frames = v;
+  }
   if (const char* se = getenv("HFG_SPLIT")) h->split = atoi(se);
   h->fmt = split_fmt(cfg->dtype);
   // bf16-valued weights: their lo plane is zero, the kernels skip lo(w) * hi(x)
@@ -2118,9 +2170,6 @@ int hfg_debug_packed_layer(hfg_handle* h, const char* mod, float* out, size_t ca
       info[9] = L.kind == L_POST ? 0
                 : L.prec == 1    ? hfg::kBf16x3Tiles[L.tile].MT()
                                  : kTiles[L.tile].MT();
-      // the exponents are set by the commit (0 while weights are missing)
-      if (h->dirty && h->fmt == hfg::kFmtF16) (void)do_commit(h);
-      info[10] = L.ew;
     }
     if (!out) return HFG_OK;
     if (h->dirty) {
@@ -2130,6 +2179,22 @@ int hfg_debug_packed_layer(hfg_handle* h, const char* mod, float* out, size_t ca
     if (cap < L.w_len + L.b_len) return fail(HFG_EINVAL, "output buffer too small");
     memcpy(out, h->packed_host.data() + L.w_off, sizeof(float) * L.w_len);
     memcpy(out + L.w_len, h->packed_host.data() + L.b_off, sizeof(float) * L.b_len);
+    return HFG_OK;
+  }
+  return fail(HFG_EINVAL, "unknown layer '%s'", mod);
+}
+
+// The f16x3 packing exponent of layer `mod` (0 in the other modes): set by the commit, so a
+// handle with uncommitted weights commits first and returns its error (e.g. weights missing).
+int hfg_debug_layer_exponent(hfg_handle* h, const char* mod, int* ew) {
+  if (!h || !mod || !ew) return fail(HFG_EINVAL, "NULL argument");
+  for (auto& L : h->layers) {
+    if (L.mod != mod) continue;
+    if (h->dirty) {
+      int rc = do_commit(h);
+      if (rc) return rc;
+    }
+    *ew = L.ew;
     return HFG_OK;
   }
   return fail(HFG_EINVAL, "unknown layer '%s'", mod);

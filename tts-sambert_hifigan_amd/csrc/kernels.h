@@ -62,6 +62,10 @@ struct ConvParams {
   const uint32_t* amax_in;
   uint32_t* amax_out;
   int ew;
+  // block stagger (tile 5): blocks of linear id in [stag_lo, stag_hi) first wait stag_n
+  // microseconds, so the co-resident blocks of a multi-round grid do not run
+  // their epilogues in lockstep (0: off)
+  int stag_lo, stag_hi, stag_n;
   int dbg;           // ablation flags (HFG_DEBUG_FLAGS, builds with -DHFG_ABLATE=1 only; wrong
                      // results when set), bf16x3 kernel: bit0 skip input restaging after the
                      // first chunk, bit2 no per-chunk barrier, bit3 no epilogue, bit7 every
@@ -260,6 +264,7 @@ struct RbParams {
   const float* post_w;   // conv_post weight [C][7] fp32
   const float* post_b;   // conv_post bias [1]
   float* wav;
+  int stag_lo, stag_hi, stag_n;  // block stagger (ConvParams)
   int dbg;               // ablations (HFG_DEBUG_FLAGS, wrong results when set): bit4 no MRF
                          // epilogue, bit5 no x loads, bit6 no operand writes
 };

@@ -66,6 +66,10 @@ struct hfg_mel_handle {
   void* tw = nullptr;
   int* band = nullptr;
   float* bw = nullptr;
+  // tables replaced by hfg_mel_set_tables: a forward still in flight on any stream may read
+  // them, so they are freed at destroy (or, past kMaxRetired, after one device sync) instead of
+  // syncing the device on every replacement
+  std::vector<void*> retired;
 };
 
 namespace {
@@ -138,13 +142,19 @@ int upload_tables(hfg_mel_handle* h, const float* win, const float* fb) {
          hipMemcpy(t.fresh, t.src, t.bytes, hipMemcpyHostToDevice) == hipSuccess;
     if (!ok) break;
   }
-  if (ok) {
-    // a forward in flight may still read the old tables
+  constexpr size_t kMaxRetired = 256;
+  if (ok && h->retired.size() + tbls.size() > kMaxRetired) {
+    // rare (hundreds of replacements): one sync retires every old table at once
     ok = hipDeviceSynchronize() == hipSuccess;
+    if (ok) {
+      for (void* p : h->retired) (void)hipFree(p);
+      h->retired.clear();
+    }
   }
   for (auto& t : tbls) {
     if (ok) {
-      if (*t.dst) (void)hipFree(*t.dst);
+      // a forward in flight may still read the old table: retired, freed at destroy
+      if (*t.dst) h->retired.push_back(*t.dst);
       *t.dst = t.fresh;
     } else if (t.fresh) {
       (void)hipFree(t.fresh);
@@ -241,6 +251,7 @@ void hfg_mel_destroy(hfg_mel_handle* h) {
   if (h->tw) (void)hipFree(h->tw);
   if (h->band) (void)hipFree(h->band);
   if (h->bw) (void)hipFree(h->bw);
+  for (void* p : h->retired) (void)hipFree(p);
   delete h;
 }
 

@@ -151,6 +151,11 @@ resblock_bf16x3(const RbParams p) {
   const int len_b = p.len ? min(p.len[b], p.L) : p.L;
   const int t0 = blockIdx.x * p.W;
   if (t0 >= len_b) return;  // whole block past this utterance's end (block-uniform)
+  if (p.stag_n > 0) {
+    const int id = blockIdx.x + gridDim.x * blockIdx.y;
+    if (id >= p.stag_lo && id < p.stag_hi)
+      stagger_wait(p.stag_n);
+  }
 #if HFG_RB_TIMING
   const int ts_region = NWIN == 256 && C == 64 ? 18 + (p.conv0 > 0 ? 1 : 0)
                         : ((KT == 3 ? 0 : KT == 7 ? 1 : 2) * 3 + (C == 32 ? 0 : C == 64 ? 1 : 2)) * 2 +
