@@ -174,3 +174,49 @@ def test_split_resblock_is_bitwise_invisible(pkg, dev, preset, precision):
             d = (outs["0" + k] - outs["1" + k]).abs().max().item()
             print(f"\n{preset} [{precision}] split vs one launch{' (conc)' if k else ''}: {d:.2e}")
             assert d <= 1e-7
+
+
+@pytest.mark.parametrize("precision", ["f16x3", "bf16x3", "bf16w"])
+@pytest.mark.parametrize("preset,B,T,lens", [("v1", 4, 1100, [1100, 513, 3, 1050]),
+                                             ("v1", 1, 3000, None),
+                                             ("nonexact", 3, 300, [300, 211, 97])])
+def test_persistent_resblock_grid_bitwise(pkg, dev, preset, B, T, lens, precision):
+    """HFG_RB_PERSIST (2, the default: a grid of n_CU blocks; 1: n_CU / stream halves): the C = 64
+    ResBlock launches with the 512-column window (one block per CU) run as a persistent grid that walks the windows and copies
+    each window's x to LDS beside the previous window's MRF round trip.  Every window's
+    arithmetic is the one-window-per-block kernel's, so the wav is bitwise unchanged: ragged
+    batches (windows past an item's end skipped), one long item (many windows per block),
+    1 and 2 streams; and within 1e-4 of the oracle."""
+    from oracle import config as C, hifigan_torch as H
+    cfg = C.PRESETS[preset]
+    sd = C.make_state_dict(cfg, seed=57)
+    mel = torch.randn(B, 80, T, generator=torch.Generator().manual_seed(T + B))
+    outs, names = {}, {}
+    for mode in ("0", "1", "2"):  # 2: a grid of every CU per half-batch stream
+        gen = _gen(pkg, cfg, sd, dev, precision, {"HFG_RB_PERSIST": mode, "HFG_RB_CONC": "0"})
+        h = gen.hip_handle(dev)
+        for n in (1, 2):
+            h.set_streams(n)
+            h.profile_reset()
+            h.set_profiling(True)
+            with torch.no_grad():
+                outs[mode, n] = gen(mel.to(dev), lengths=lens)
+            torch.cuda.synchronize()
+            h.set_profiling(False)
+            names[mode, n] = h.profile_summary()
+    assert any("persist" in k for k in names["1", 1]), names["1", 1]
+    assert not any("persist" in k for k in names["0", 1])
+    for n in (1, 2):
+        for m in ("1", "2"):
+            assert torch.equal(outs["0", n], outs[m, n]), (m, n, (outs["0", n] - outs[m, n]).abs().max())
+    if precision != "bf16w":
+        b = 0
+        n = T if lens is None else lens[0]
+        a, e = min(200, n // 2), min(200, n // 2) + 40
+        ref = H.generator_forward(H.to_torch_state(sd), cfg, mel[b:b + 1, :, max(0, a - 15):e + 15])
+        hop = C.out_len(cfg, 2) - C.out_len(cfg, 1)
+        off = (a - max(0, a - 15)) * hop
+        if C.out_len(cfg, 7) == 7 * hop:
+            got = outs["1", 1][b:b + 1, :, a * hop:e * hop].cpu()
+            assert (got - ref[:, :, off:off + (e - a) * hop]).abs().max().item() < ATOL
+

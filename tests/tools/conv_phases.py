@@ -51,6 +51,11 @@ def main():
     buf = np.zeros(REGIONS * BLOCKS * SLOTS, dtype=np.uint64)
     assert dl.hfg_debug_cv_ts(buf.ctypes.data_as(ctypes.c_void_p), ctypes.c_size_t(buf.nbytes)) == 0
     buf = buf.reshape(REGIONS, BLOCKS, SLOTS).astype(np.int64)
+    odir = os.path.join(ROOT, "gpurun_out", "r05")
+    os.makedirs(odir, exist_ok=True)
+    tag = os.environ.get("CVP_TAG", "default")
+    # raw stamps (slot 12: HW_ID | XCC_ID << 32 of the block's wave 0) for offline analysis
+    np.save(os.path.join(odir, f"cvp_raw_{tag}.npy"), buf[:9])
     out = {}
     for r, (kt, epi) in enumerate((k, e) for k in (3, 7, 11, 0) for e in ("plain", "res", "res+mrf")):
         blk = buf[r]
@@ -77,7 +82,7 @@ def main():
                                    for q in (25, 50, 75, 100)]}
         out[f"k{kt} {epi}"] = row
         print(f"k{kt} {epi}", json.dumps(row))
-    with open(os.path.join(ROOT, "gpurun_out", "r04", "conv_phases.json"), "w") as f:
+    with open(os.path.join(odir, f"conv_phases_{tag}.json"), "w") as f:
         json.dump(out, f, indent=1)
 
 

@@ -401,6 +401,9 @@ conv1d_bf16x3(const ConvParams p) {
   auto cstamp = [&](int i) { tsv[i] = __builtin_amdgcn_s_memtime(); };
   uint64_t bar_wait = 0;
   tsv[0] = __builtin_amdgcn_s_memrealtime();
+  // placement: HW_ID (CU, SE, SIMD, wave) and XCC of wave 0
+  tsv[12] = (uint64_t)__builtin_amdgcn_s_getreg((31 << 11) | 4) |
+            ((uint64_t)__builtin_amdgcn_s_getreg((31 << 11) | 20) << 32);
   cstamp(1);
 #else
   auto cstamp = [](int) {};

@@ -4,6 +4,7 @@
 // management and the 78-launch forward schedule of
 // HiFiGANGenerator.forward (models/hifigan.py:224-261).
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 
 #include <algorithm>
 #include <cmath>
@@ -185,6 +186,14 @@ struct hfg_handle {
   // HFG_STAGGER="conv,rb": microseconds the first round's second-half blocks in the
   // multi-round tile-5 layer-conv and whole-ResBlock grids wait (experiment; 0 = off)
   int stag_conv = 0, stag_rb = 0;
+  // HFG_RB_PERSIST (default 2): persistent grids for the one-block-per-CU ResBlock launches
+  int rb_persist = 2;
+  int n_cu = 256;      // compute units of the device (hipDeviceAttributeMultiprocessorCount)
+  int halves = 1;      // batch halves of the running forward (2: two streams share the CUs)
+  // HFG_CU_SPLIT="1[,delay_us]" (experiment): the two batch halves on streams masked to
+  // disjoint halves of the CUs, the second half started delay_us later
+  int cu_split = 0, cu_delay = 0;
+  hipStream_t cu_s[2] = {nullptr, nullptr};
   // batch split over two HIP streams (HFG_SPLIT=1 disables): the two halves' launches
   // overlap, so one half's ramp-down / epilogue tail runs beside the other's main loops
   int split = 2;
@@ -1170,9 +1179,15 @@ int run_resblock(hfg_handle* h, Launcher& ln, const RbFused& rb, const float* x,
     p.mrf_rcp = hfg::fast_div_ok(mrf_div) ? 1.0f / mrf_div : 0.0f;
     p.amax_out = last ? aout : nullptr;
     p.dbg = h->dbg_flags;
+    // resident blocks per CU from the LDS footprint
+    const int per_cu = hfg::rb_lds_bytes(C, rb.nwin, n_all) <= 80 * 1024 ? 2 : 1;
+    // a persistent grid of the resident blocks (each window's x load overlaps the previous
+    // window's MRF round trip; launch_resblock_bf16x3 runs it where a persistent variant is
+    // built, C = 64 with the 512-column window).  HFG_RB_PERSIST: 0 off, 1 one block per CU
+    // of the half-batch stream's share (n_CU / halves), 2 one per CU
+    if (h->rb_persist && per_cu == 1 && !(last && post))
+      p.persist = std::max(1, h->n_cu / (h->rb_persist == 1 ? h->halves : 1));
     if (h->stag_rb > 0) {
-      // resident blocks per CU from the LDS footprint (256 CUs)
-      const int per_cu = hfg::rb_lds_bytes(C, rb.nwin, n_all) <= 80 * 1024 ? 2 : 1;
       const int64_t blocks = (Lt + p.W - 1) / p.W * B;
       if (blocks >= 2 * 256 * per_cu) {
         p.stag_lo = 128 * per_cu;
@@ -1636,7 +1651,8 @@ int forward_split(hfg_handle* h, const float* mel, int64_t B, int64_t T,
                   const hfg_forward_opts* o, float* wav, int64_t out_len, void* ws, size_t ws_len,
                   hipStream_t stream) {
   ++h->fwd_count;
-  if (!split_batch(h, B, T))
+  h->halves = split_batch(h, B, T) ? 2 : 1;
+  if (h->halves == 1)
     return forward_impl(h, mel, B, T, o, wav, out_len, ws, ws_len, stream, 0, nullptr, true);
   if (B <= 0 || T <= 0) return fail(HFG_EINVAL, "B and T must be > 0");
   if (ws_len < ws_bytes_for(h, B, T)) return fail(HFG_EINVAL, "workspace too small");
@@ -1648,11 +1664,35 @@ int forward_split(hfg_handle* h, const float* mel, int64_t B, int64_t T,
   }
   const int64_t B1 = (B + 1) / 2, B2 = B - B1;
   const size_t w1 = ws_part_bytes(h, B1, T);
+  hipStream_t s0 = stream, s1 = h->aux;
+  if (h->cu_split && h->device >= 0) {
+    if (!h->cu_s[0]) {
+      const int nw = (h->n_cu + 31) / 32;
+      for (int k = 0; k < 2; ++k) {
+        std::vector<uint32_t> mask(nw, 0u);
+        for (int c = k * h->n_cu / 2; c < (k + 1) * h->n_cu / 2; ++c) mask[c / 32] |= 1u << (c % 32);
+        hipError_t e = hipExtStreamCreateWithCUMask(&h->cu_s[k], (uint32_t)nw, mask.data());
+        if (e != hipSuccess) return hip_fail(e, "create CU-masked stream");
+      }
+    }
+    s0 = h->cu_s[0];
+    s1 = h->cu_s[1];
+  }
   hipError_t e = hipEventRecord(h->fork_ev, stream);
-  if (e == hipSuccess) e = hipStreamWaitEvent(h->aux, h->fork_ev, 0);
+  if (e == hipSuccess) e = hipStreamWaitEvent(s1, h->fork_ev, 0);
+  if (e == hipSuccess && s0 != stream) e = hipStreamWaitEvent(s0, h->fork_ev, 0);
   if (e != hipSuccess) return hip_fail(e, "fork");
-  int rc = forward_impl(h, mel, B1, T, o, wav, out_len, ws, w1, stream, 0);
+  if (h->cu_split && h->cu_delay > 0) {
+    e = hfg::launch_spin(h->cu_delay, s1);
+    if (e != hipSuccess) return hip_fail(e, "spin");
+  }
+  int rc = forward_impl(h, mel, B1, T, o, wav, out_len, ws, w1, s0, 0);
   if (rc) return rc;
+  if (s0 != stream) {
+    e = hipEventRecord(h->fork_ev, s0);
+    if (e == hipSuccess) e = hipStreamWaitEvent(stream, h->fork_ev, 0);
+    if (e != hipSuccess) return hip_fail(e, "join");
+  }
   hfg_forward_opts o2{};
   if (o) {
     o2 = *o;
@@ -1660,8 +1700,8 @@ int forward_split(hfg_handle* h, const float* mel, int64_t B, int64_t T,
   }
   rc = forward_impl(h, mel + (size_t)B1 * h->cfg.n_mels * T, B2, T, o ? &o2 : nullptr,
                     wav + (size_t)B1 * out_len, out_len, static_cast<char*>(ws) + w1,
-                    ws_len - w1, h->aux, 1);
-  e = hipEventRecord(h->join_ev, h->aux);
+                    ws_len - w1, s1, 1);
+  e = hipEventRecord(h->join_ev, s1);
   if (e == hipSuccess) e = hipStreamWaitEvent(stream, h->join_ev, 0);
   if (e != hipSuccess) return hip_fail(e, "join");
   return rc;
@@ -1687,6 +1727,14 @@ int create_impl(const hfg_config* cfg, bool mrf_only, int device, hfg_handle** o
   if (const char* dbg = getenv("HFG_DEBUG_FLAGS")) h->dbg_flags = atoi(dbg);
 #endif
   if (const char* sg = getenv("HFG_STAGGER")) sscanf(sg, "%d,%d", &h->stag_conv, &h->stag_rb);
+  if (const char* rp = getenv("HFG_RB_PERSIST")) h->rb_persist = std::min(2, std::max(0, atoi(rp)));
+  if (const char* cs = getenv("HFG_CU_SPLIT")) sscanf(cs, "%d,%d", &h->cu_split, &h->cu_delay);
+  if (device >= 0) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess &&
+        n > 0)
+      h->n_cu = n;
+  }
   // knobs of earlier rounds' schedules that no longer exist: say so instead of silently
   // running the default schedule under a variant's label
   {
@@ -1791,6 +1839,8 @@ void hfg_destroy(hfg_handle* h) {
       if (h->fork_ev) (void)hipEventDestroy(h->fork_ev);
       if (h->join_ev) (void)hipEventDestroy(h->join_ev);
       if (h->aux) (void)hipStreamDestroy(h->aux);
+      for (auto& cs : h->cu_s)
+        if (cs) (void)hipStreamDestroy(cs);
       for (int part = 0; part < 2; ++part) {
         if (h->rb_fork[part]) (void)hipEventDestroy(h->rb_fork[part]);
         for (int j = 0; j < HFG_MAX_RES; ++j) {
@@ -1991,6 +2041,7 @@ int mrf_run(hfg_handle* h, int only_j, const float* x, int64_t B, int64_t L, flo
   if (!g.ok) return fail(HFG_ENODEV, "hipSetDevice(%d) failed", h->device);
   if (h->dirty && (rc = do_commit(h))) return rc;
   ++h->fwd_count;
+  h->halves = 1;
   const size_t one = (mrf_ws_bytes(h, B, L) - slots_bytes(h, B)) / 2;
   float* R = static_cast<float*>(ws);
   float* Tb = R + one / sizeof(float);
@@ -2244,6 +2295,7 @@ int hfg_forward_taps(hfg_handle* h, const float* mel, int64_t B, int64_t T, floa
     if (rc) return rc;
   }
   ++h->fwd_count;
+  h->halves = 1;
   return forward_impl(h, mel, B, T, nullptr, wav, out_len, workspace, workspace_bytes,
                       reinterpret_cast<hipStream_t>(stream), 0, taps, !split_batch(h, B, T));
 }

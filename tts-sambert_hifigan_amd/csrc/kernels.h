@@ -265,6 +265,11 @@ struct RbParams {
   const float* post_b;   // conv_post bias [1]
   float* wav;
   int stag_lo, stag_hi, stag_n;  // block stagger (ConvParams)
+  int batch;             // items (set by launch_resblock_bf16x3)
+  // persistent grid (one-block-per-CU instances; not with the fused conv_post): 0 = one window
+  // per block, else the launch runs min(windows, persist) blocks that walk the windows and
+  // overlap each window's MRF read-modify-write with the next window's x loads
+  int persist;
   int dbg;               // ablations (HFG_DEBUG_FLAGS, wrong results when set): bit4 no MRF
                          // epilogue, bit5 no x loads, bit6 no operand writes
 };
@@ -273,6 +278,8 @@ struct RbParams {
 inline bool fast_div_ok(float d) {
   return d == 1.f || d == 2.f || d == 3.f || d == 4.f || d == 5.f || d == 7.f || d == 8.f;
 }
+// one wave spinning `us` microseconds on `stream` (schedule experiments: a delayed stream)
+hipError_t launch_spin(int us, hipStream_t stream);
 bool rb_supported(int C, int kt, int nwin, int wm);
 size_t rb_lds_bytes(int C, int nwin, int n_conv);
 hipError_t launch_resblock_bf16x3(int C, int nwin, int wm, int kt, int fmt, int np,

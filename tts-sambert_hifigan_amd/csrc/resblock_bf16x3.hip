@@ -33,6 +33,7 @@
 // passes per dilation for the layer-per-launch schedule.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <mutex>
 
 #include <cstdio>
@@ -111,7 +112,7 @@ __device__ __forceinline__ void conv_post_tail(const RbParams& p, const floatx16
   }
 }
 
-template <int KT, int WAVES_M, int WAVES_N, int WM, int NP, int FMT>
+template <int KT, int WAVES_M, int WAVES_N, int WM, int NP, int FMT, bool PERSIST>
 __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N, 2)  // 2 waves/SIMD: <= 256 VGPRs
 resblock_bf16x3(const RbParams p) {
   constexpr int NW = WAVES_M * WAVES_N;
@@ -147,15 +148,34 @@ resblock_bf16x3(const RbParams p) {
   const int wave_n = wave / WAVES_M;
   const int half = lane >> 5;
   const int col = lane & 31;
-  const int b = blockIdx.y;
-  const int len_b = p.len ? min(p.len[b], p.L) : p.L;
-  const int t0 = blockIdx.x * p.W;
-  if (t0 >= len_b) return;  // whole block past this utterance's end (block-uniform)
+  // ---- windows: w = tile + n_tiles * item.  One window per block (grid n_tiles x B), or
+  // with p.persist a grid of G blocks that walks the windows w, w + G, w + 2G, ... and issues
+  // the next window's x and margin loads beside the current window's MRF read-modify-write
+  // (one-block-per-CU instances: nothing else on the CU hides those round trips).  Windows past
+  // an item's length are skipped (block-uniform). ----
+  const int n_tiles = (p.L + p.W - 1) / p.W;
+  const int n_win = n_tiles * p.batch;
+  const int wstride = PERSIST ? (int)gridDim.x : n_win;
+  auto item_of = [&](int wi) { return __builtin_amdgcn_readfirstlane(wi / n_tiles); };
+  auto len_of = [&](int bi) { return p.len ? min(p.len[bi], p.L) : p.L; };
+  auto valid = [&](int wi) {
+    const int bi = item_of(wi);
+    return (wi - bi * n_tiles) * p.W < len_of(bi);
+  };
+  int w = PERSIST ? (int)blockIdx.x : (int)(blockIdx.x + n_tiles * blockIdx.y);
+  while (w < n_win && !valid(w)) {
+    if (!PERSIST) return;  // whole block past this utterance's end (block-uniform)
+    w += wstride;
+  }
+  if (w >= n_win) return;
   if (p.stag_n > 0) {
     const int id = blockIdx.x + gridDim.x * blockIdx.y;
     if (id >= p.stag_lo && id < p.stag_hi)
       stagger_wait(p.stag_n);
   }
+  int b = item_of(w);
+  int len_b = len_of(b);
+  int t0 = (w - b * n_tiles) * p.W;
 #if HFG_RB_TIMING
   const int ts_region = NWIN == 256 && C == 64 ? 18 + (p.conv0 > 0 ? 1 : 0)
                         : ((KT == 3 ? 0 : KT == 7 ? 1 : 2) * 3 + (C == 32 ? 0 : C == 64 ? 1 : 2)) * 2 +
@@ -164,7 +184,7 @@ resblock_bf16x3(const RbParams p) {
   uint64_t* const ts = g_rb_ts + ((size_t)ts_region * kRbTsBlocks + (ts_blk < kRbTsBlocks ? ts_blk : 0)) * kRbTsSlots;
   // stamps kept in LDS (past the f16x3 maxima) and stored once at the end: a global (or
   // scratch) store mid-kernel would make every later vmcnt wait also wait for its write (one
-  // in-order queue for vector loads and stores)
+  // in-order queue for vector loads and stores).  A persistent block keeps its last window's.
   uint64_t* const tsv = reinterpret_cast<uint64_t*>(amax_s + 16);
   auto stamp = [&](int i) {
     const uint64_t t = __builtin_amdgcn_s_memtime();
@@ -177,7 +197,7 @@ resblock_bf16x3(const RbParams p) {
 #else
   auto stamp = [](int) {};
 #endif
-  const int ws = t0 - p.halo;
+  int ws = t0 - p.halo;
   const int cbase = wave_n * 32 * WN;      // first window column of this wave
   const int row0 = wave_m * 32 * WM;     // first row of this wave (WM row tiles of 32)
   const int n_conv = p.n_conv;
@@ -191,8 +211,11 @@ resblock_bf16x3(const RbParams p) {
   for (int i = tid; i < n_conv * C; i += NT) bias_s[i] = p.bias[i];
 
   bool vk[WN];
+  auto set_vk = [&]() {
 #pragma unroll
-  for (int k = 0; k < WN; ++k) vk[k] = (unsigned)(ws + cbase + 32 * k + col) < (unsigned)len_b;
+    for (int k = 0; k < WN; ++k) vk[k] = (unsigned)(ws + cbase + 32 * k + col) < (unsigned)len_b;
+  };
+  set_vk();
 
   // ---- A stream (buffer loads: SGPR descriptor + scalar step offset, no address VALU) ----
   const __amdgpu_buffer_rsrc_t wrs =
@@ -221,25 +244,28 @@ resblock_bf16x3(const RbParams p) {
   // ABI's bound: a dword is dropped when voffset + soffset + 4 passes num_records, so a
   // 4-GiB item would lose its last float), so every offset and its dword end fit 32 bits;
   // the range is never relied on otherwise (masked lanes read offset 0).
-  const unsigned Lb = (unsigned)p.L * 4u;
+  unsigned Lb = (unsigned)p.L * 4u;
   auto srow = [&](int i, int r) { return (unsigned)(row0 + 32 * i + (r & 3) + 8 * (r >> 2)) * Lb; };
   const unsigned lrow = 4u * (unsigned)half * (unsigned)p.L;
   const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(p.x + (int64_t)b * p.bs), 0, (int)0xFFFFFFFFu, 0x00020000);
 
-  // ---- residual stream x: window -> registers (zero outside [0, len)) ----
+  // ---- residual stream x: window -> registers (zero outside [0, len): masked after the wait) ----
   floatx16 xcur[WM][WN];
-  {
+  auto issue_x = [&](floatx16 (&dst)[WM][WN], const __amdgpu_buffer_rsrc_t& rs, int wsx, int lenx) {
 #pragma unroll
     for (int k = 0; k < WN; ++k) {
-      const unsigned vo = vk[k] ? (lrow + (unsigned)(ws + cbase + 32 * k + col)) * 4u : 0u;
+      const int gc = wsx + cbase + 32 * k + col;
+      const unsigned vo = (unsigned)gc < (unsigned)lenx ? (lrow + (unsigned)gc) * 4u : 0u;
 #pragma unroll
       for (int i = 0; i < WM; ++i)
 #pragma unroll
         for (int r = 0; r < 16; ++r)
-          xcur[i][k][r] = __builtin_bit_cast(
-              float, __builtin_amdgcn_raw_buffer_load_b32(xrs, (int)vo, (int)srow(i, r), 0));
+          dst[i][k][r] = __builtin_bit_cast(
+              float, __builtin_amdgcn_raw_buffer_load_b32(rs, (int)vo, (int)srow(i, r), 0));
     }
+  };
+  auto mask_x = [&]() {
     // ablation bit 5 zeroes x after the loads (a select on a uniform flag inside the load
     // expression made the compiler branch per element)
     const bool xz = kAblate && (dbg & 32);
@@ -249,6 +275,42 @@ resblock_bf16x3(const RbParams p) {
       for (int k = 0; k < WN; ++k)
 #pragma unroll
         for (int r = 0; r < 16; ++r) xcur[i][k][r] = (vk[k] && !xz) ? xcur[i][k][r] : 0.f;
+  };
+  // ---- persistent grid: a window's x [C][ROWS] (columns ws - MARG ..) goes to the operand
+  // planes' LDS by buffer-load-to-LDS (no VGPRs), issued beside the previous window's MRF
+  // read-modify-write; the window then reads its x and margins from LDS.  The item's buffer
+  // range (C * L floats) turns the columns outside it into zeros; columns outside [0, len)
+  // are masked as in the register path. ----
+  constexpr int XD_N = C * ROWS / 64;  // 64-dword pieces (ROWS % 4 == 0: C * ROWS % 64 == 0)
+  static_assert(C * ROWS % 64 == 0 && C * ROWS * 4 == NG * GS, "x copy fills the operand planes");
+  constexpr int XD_T = (XD_N + NW - 1) / NW;
+  auto dma_x = [&](int wsx, int bi) {
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(p.x + (int64_t)bi * p.bs), 0, (int)(C * Lb), 0x00020000);
+    int c = (wave * 64 + lane) / ROWS;
+    int cl = wave * 64 + lane - c * ROWS;
+#pragma unroll 4
+    for (int q = 0; q < XD_T; ++q) {
+      const int j = wave + NW * q;
+      if (j < XD_N) {
+        const unsigned vo = ((unsigned)c * (unsigned)p.L + (unsigned)(wsx - MARG + cl)) * 4u;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_ptr_t3)(lds + j * 256), 4, (int)vo, 0, 0,
+                                                 0);
+      }
+      static_assert(64 * NW < 3 * ROWS, "two wraps at most");
+      cl += 64 * NW;
+      c += cl >= ROWS ? 1 : 0;
+      cl -= cl >= ROWS ? ROWS : 0;
+      c += cl >= ROWS ? 1 : 0;
+      cl -= cl >= ROWS ? ROWS : 0;
+    }
+  };
+  if constexpr (PERSIST) {
+    dma_x(ws, b);
+    wait_vm<0>();
+    lds_barrier();
+  } else {
+    issue_x(xcur, xrs, ws, len_b);
   }
   // ---- the first conv's margins: operand columns [-R0, 0) and [NWIN, NWIN + R0) of the
   // window read from x (R0 = that conv's receptive-field radius <= MARG, host-checked), so the
@@ -258,46 +320,82 @@ resblock_bf16x3(const RbParams p) {
   const int R0 = (KT - 1) / 2 * p.dil[0];
   const int n_mg = 4 * R0 * NG;
   float mg[MG_T][8];
-  bool mg_ok[MG_T];
-  int mg_off[MG_T];  // byte offset of the task's 16-B row in the hi plane
-#pragma unroll
-  for (int q = 0; q < MG_T; ++q) {
+  auto mg_col = [&](int q, int wsx) {  // global column of margin task q (window origin wsx)
     const int t = tid + q * NT;
-    const int hh = t & 1, gq = (t >> 1) % NG, m = (t >> 1) / NG;
-    const int c = m < R0 ? m - R0 : NWIN + m - R0;  // window column
-    const int gc = ws + c;
-    const bool ok = t < n_mg && (unsigned)gc < (unsigned)len_b;
-    mg_ok[q] = ok;
-    mg_off[q] = gq * GS + hh * HPS + (c + MARG) * 16;
-    const unsigned vo = ok ? ((unsigned)(16 * gq + 4 * hh) * (unsigned)p.L + (unsigned)gc) * 4u : 0u;
+    const int m = (t >> 1) / NG;
+    return wsx + (m < R0 ? m - R0 : NWIN + m - R0);
+  };
+  auto issue_mg = [&](float (&dst)[MG_T][8], const __amdgpu_buffer_rsrc_t& rs, int wsx, int lenx) {
 #pragma unroll
-    for (int e = 0; e < 8; ++e)
-      mg[q][e] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
-                                               xrs, (int)vo, (int)(((e & 3) + 8 * (e >> 2)) * Lb), 0));
-  }
+    for (int q = 0; q < MG_T; ++q) {
+      const int t = tid + q * NT;
+      const int hh = t & 1, gq = (t >> 1) % NG;
+      const int gc = mg_col(q, wsx);
+      const bool ok = t < n_mg && (unsigned)gc < (unsigned)lenx;
+      const unsigned vo = ok ? ((unsigned)(16 * gq + 4 * hh) * (unsigned)p.L + (unsigned)gc) * 4u : 0u;
 #pragma unroll
-  for (int q = 0; q < MG_T; ++q)
+      for (int e = 0; e < 8; ++e)
+        dst[q][e] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                                  rs, (int)vo, (int)(((e & 3) + 8 * (e >> 2)) * Lb), 0));
+    }
+  };
+  auto mask_mg = [&]() {
 #pragma unroll
-    for (int e = 0; e < 8; ++e) mg[q][e] = mg_ok[q] ? mg[q][e] : 0.f;
+    for (int q = 0; q < MG_T; ++q) {
+      const int gc = mg_col(q, ws);
+      const bool ok = tid + q * NT < n_mg && (unsigned)gc < (unsigned)len_b;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) mg[q][e] = ok ? mg[q][e] : 0.f;
+    }
+  };
+  if constexpr (!PERSIST) issue_mg(mg, xrs, ws, len_b);
+  // persistent grid: x and the margins from the LDS copy
+  auto read_x_lds = [&]() {
+    const float* xl = reinterpret_cast<const float*>(lds);
+    // the lane's base index, opaque per window: the loop-invariant addresses of the 16 x WM x WN
+    // elements would otherwise be hoisted out of the window loop and held in VGPRs across it
+    int xb = (row0 + 4 * half) * ROWS + MARG + cbase + col;
+    asm volatile("" : "+v"(xb));
+#pragma unroll
+    for (int k = 0; k < WN; ++k)
+#pragma unroll
+      for (int i = 0; i < WM; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          xcur[i][k][r] = xl[xb + (32 * i + (r & 3) + 8 * (r >> 2)) * ROWS + 32 * k];
+#pragma unroll
+    for (int q = 0; q < MG_T; ++q) {
+      const int t = min(tid + q * NT, n_mg > 0 ? n_mg - 1 : 0);
+      const int hh = t & 1, gq = (t >> 1) % NG, m = (t >> 1) / NG;
+      const int cw = MARG + (m < R0 ? m - R0 : NWIN + m - R0);
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        mg[q][e] = xl[(16 * gq + 4 * hh + (e & 3) + 8 * (e >> 2)) * ROWS + cw];
+    }
+  };
   auto write_margins = [&](float sc) {
 #pragma unroll
     for (int q = 0; q < MG_T; ++q) {
-      if (tid + q * NT < n_mg) {
+      const int t = tid + q * NT;
+      if (t < n_mg) {
+        const int hh = t & 1, gq = (t >> 1) % NG, m = (t >> 1) / NG;
+        const int c = m < R0 ? m - R0 : NWIN + m - R0;  // window column
+        const int off = gq * GS + hh * HPS + (c + MARG) * 16;
         bf16x8 h, l;
 #pragma unroll
         for (int e = 0; e < 8; e += 2) {
           floatx2 a;
           a[0] = fmaxf(mg[q][e] * sc, mg[q][e] * (kLReluSlope * sc));
           a[1] = fmaxf(mg[q][e + 1] * sc, mg[q][e + 1] * (kLReluSlope * sc));
-          bf16x2 hh, ll;
-          split2<FMT>(a, hh, ll);
-          h[e] = hh[0];
-          h[e + 1] = hh[1];
+          bf16x2 hh2, ll;
+          split2<FMT>(a, hh2, ll);
+          h[e] = hh2[0];
+          h[e + 1] = hh2[1];
           l[e] = ll[0];
           l[e + 1] = ll[1];
         }
-        *reinterpret_cast<bf16x8*>(lds + mg_off[q]) = h;
-        *reinterpret_cast<bf16x8*>(lds + mg_off[q] + PS) = l;
+        *reinterpret_cast<bf16x8*>(lds + off) = h;
+        *reinterpret_cast<bf16x8*>(lds + off + PS) = l;
       }
     }
   };
@@ -370,30 +468,9 @@ resblock_bf16x3(const RbParams p) {
   auto block_exp = [&]() {
     float m = amax_s[0];
 #pragma unroll
-    for (int w = 1; w < NW; ++w) m = fmaxf(m, amax_s[w]);
+    for (int w_ = 1; w_ < NW; ++w_) m = fmaxf(m, amax_s[w_]);
     return x3_exp(m);
   };
-  int ex = 0;
-  int radius = 0;  // f16x3: receptive-field radius of the convs run so far
-  if constexpr (FMT == kFmtF16) {
-#if HFG_RB_TIMING
-    wait_vm<0>();
-    stamp(21);
-#endif
-    float mm = 0.f;  // the margin columns are part of the first operand
-#pragma unroll
-    for (int q = 0; q < MG_T; ++q)
-#pragma unroll
-      for (int e = 0; e < 8; ++e) mm = fmaxf(mm, fabsf(mg[q][e]));
-    wave_amax(xcur, 0, mm);
-    lds_barrier();
-    ex = block_exp();
-    stamp(22);
-  }
-  write_operand(xcur, exp2i(ex));
-  write_margins(exp2i(ex));
-  lds_barrier();
-  stamp(2);
 
   // conv cv over the whole window: acc = bias + W_cv * operand (one LDS barrier at the
   // end: every wave has read the operand, which the caller then overwrites in place)
@@ -413,8 +490,8 @@ resblock_bf16x3(const RbParams p) {
     bf16x8 bh[2][WN], bl[2][WN];
     // step s = (group g, tap j): rows shifted by j*d - pad, one VALU add per step,
     // tiles / planes by immediate offsets
-    auto load_b = [&](int buf, int s) {
-      const int g = s / KT, j = s - (s / KT) * KT;
+    auto load_b = [&](int buf, int s_) {
+      const int g = s_ / KT, j = s_ - (s_ / KT) * KT;
       const char* src = lds + vb + (g * GS + (j * d - pad) * 16);
 #pragma unroll
       for (int k = 0; k < WN; ++k) {
@@ -429,9 +506,9 @@ resblock_bf16x3(const RbParams p) {
     // software pipeline: B fragments one step ahead (interleaved with this step's
     // MFMAs), A fragments two steps ahead
 #pragma unroll
-    for (int s = 0; s < STEPS; ++s) {
-      const int cur = s & 1;
-      if (s + 1 < STEPS) load_b(cur ^ 1, s + 1);
+    for (int s_ = 0; s_ < STEPS; ++s_) {
+      const int cur = s_ & 1;
+      if (s_ + 1 < STEPS) load_b(cur ^ 1, s_ + 1);
 #pragma unroll
       for (int k = 0; k < WN; ++k)
 #pragma unroll
@@ -441,8 +518,8 @@ resblock_bf16x3(const RbParams p) {
           acc[i][k] = mfma32<FMT>(ra_h[cur][i], bl[cur][k], acc[i][k]);
           acc[i][k] = mfma32<FMT>(ra_h[cur][i], bh[cur][k], acc[i][k]);
         }
-      load_a(cur, qb + s + 2);
-      if (s + 1 < STEPS) {
+      load_a(cur, qb + s_ + 2);
+      if (s_ + 1 < STEPS) {
 #pragma unroll
         for (int i = 0; i < 2 * WN; ++i) {
           __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // 1 MFMA
@@ -456,6 +533,7 @@ resblock_bf16x3(const RbParams p) {
     }
   };
   // f16x3: acc = acc * 2^-(e_x + e_w) + bias (exact unscale, one rounding for the bias)
+  int ex = 0;
   auto finalize = [&](int cv) {
     const float inv = exp2i(-(ex + p.ew[cv]));
 #pragma unroll
@@ -468,162 +546,227 @@ resblock_bf16x3(const RbParams p) {
       }
   };
 
-  // dilation pairs: xt = lrelu(conv1(lrelu(x)) + b1); x = x + (conv2(xt) + b2)
-  if constexpr (FMT == kFmtBf16) {
-    for (int cv = 0; cv < n_conv; cv += 2) {
-      run_conv(cv);
-      lds_barrier();
-      write_operand(acc, 1.0f);
-      lds_barrier();
-      run_conv(cv + 1);
-      lds_barrier();
-#pragma unroll
-      for (int i = 0; i < WM; ++i)
-#pragma unroll
-        for (int k = 0; k < WN; ++k)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) xcur[i][k][r] = xcur[i][k][r] + acc[i][k][r];
-      if (cv + 2 < n_conv) {
-        write_operand(xcur, 1.0f);
-        lds_barrier();
-      }
-    }
-  } else {
-    for (int cv = 0; cv < n_conv; cv += 2) {
-      run_conv(cv);
-      stamp(3 + 2 * cv);
-      finalize(cv);
-      if (cv > 0) radius += (KT - 1) / 2 * p.dil[cv];  // conv 0: exact (margins from x)
-      wave_amax(acc, radius);
-      lds_barrier();  // every wave is done reading the operand; the maxima are posted
-      ex = block_exp();
-      write_operand(acc, exp2i(ex));
-      lds_barrier();
-      stamp(4 + 2 * cv);
-      run_conv(cv + 1);
-      stamp(5 + 2 * cv);
-      finalize(cv + 1);
-      radius += (KT - 1) / 2;  // conv2: dilation 1
-#pragma unroll
-      for (int i = 0; i < WM; ++i)
-#pragma unroll
-        for (int k = 0; k < WN; ++k)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) xcur[i][k][r] = xcur[i][k][r] + acc[i][k][r];
-      if (cv + 2 < n_conv) {
-        wave_amax(xcur, radius);
-        lds_barrier();
-        ex = block_exp();
-        write_operand(xcur, exp2i(ex));
-        lds_barrier();
-      }
-      stamp(6 + 2 * cv);
-    }
-  }
-
-  // ---- MRF: (mrf + x) [/ n_res] on the window centre ----
-  if (kAblate && (dbg & 16)) {  // ablation: no MRF epilogue
-    if (xcur[0][0][0] == 1.2345e-30f) p.mrf[0] = xcur[WM - 1][WN - 1][15];
-    return;
-  }
-  const __amdgpu_buffer_rsrc_t mrs = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)(p.mrf + (int64_t)b * p.bs), 0, (int)0xFFFFFFFFu, 0x00020000);
   const bool add = p.mrf_mode & 1;
   const bool div = p.mrf_mode & 2;
   // fused conv_post (C = 32, the network's last MRF write): the stage output is not stored;
   // it is computed on the centre plus the conv's radius 3 on either side and consumed from LDS
   const bool post = C == 32 && p.wav != nullptr;
   const int c_lo = post ? p.halo - 3 : p.halo, c_hi = post ? p.halo + p.W + 3 : p.halo + p.W;
-  bool ok[WN];
-  unsigned vo[WN];
-#pragma unroll
-  for (int k = 0; k < WN; ++k) {
-    const int c = cbase + 32 * k + col;
-    ok[k] = vk[k] && c >= c_lo && c < c_hi;
-    vo[k] = ok[k] ? (lrow + (unsigned)(ws + c)) * 4u : 0u;
-  }
-  // every MRF load is issued before any use (one wait for all 16 x WN), then the adds /
-  // divisions for every tile; the empty asm keeps the compiler from sinking a tile's loads
-  // into its store branch (which serialised one HBM round trip per element)
-  if (add) {
-    float mv[WM][WN][16];
-#pragma unroll
-    for (int i = 0; i < WM; ++i)
-#pragma unroll
-      for (int k = 0; k < WN; ++k)
-#pragma unroll
-        for (int r = 0; r < 16; ++r)
-          mv[i][k][r] = __builtin_bit_cast(
-              float, __builtin_amdgcn_raw_buffer_load_b32(mrs, (int)vo[k], (int)srow(i, r), 0));
+  for (;;) {
+    // persistent grid: the row offsets (16 x WM scalars) stay per-window values instead of
+    // being hoisted out of the window loop and held (spilled) across it
+    if constexpr (PERSIST) asm volatile("" : "+s"(Lb));
+    // ---- this window's x (in flight, or in LDS) -> operand ----
+    if constexpr (PERSIST) read_x_lds();
+    mask_x();
+    mask_mg();
+    int radius = 0;  // f16x3: receptive-field radius of the convs run so far
+    if constexpr (FMT == kFmtF16) {
 #if HFG_RB_TIMING
-    wait_vm<0>();
-    stamp(23);
+      wait_vm<0>();
+      stamp(21);
 #endif
+      float mm = 0.f;  // the margin columns are part of the first operand
 #pragma unroll
-    for (int i = 0; i < WM; ++i)
+      for (int q = 0; q < MG_T; ++q)
 #pragma unroll
-      for (int k = 0; k < WN; ++k)
+        for (int e = 0; e < 8; ++e) mm = fmaxf(mm, fabsf(mg[q][e]));
+      wave_amax(xcur, 0, mm);
+      lds_barrier();
+      ex = block_exp();
+      stamp(22);
+    } else if (PERSIST) {
+      lds_barrier();  // every wave has read x from LDS (the copy the operand overwrites)
+    }
+    write_operand(xcur, exp2i(ex));
+    write_margins(exp2i(ex));
+    lds_barrier();
+    stamp(2);
+
+    // dilation pairs: xt = lrelu(conv1(lrelu(x)) + b1); x = x + (conv2(xt) + b2)
+    if constexpr (FMT == kFmtBf16) {
+      for (int cv = 0; cv < n_conv; cv += 2) {
+        run_conv(cv);
+        lds_barrier();
+        write_operand(acc, 1.0f);
+        lds_barrier();
+        run_conv(cv + 1);
+        lds_barrier();
 #pragma unroll
-        for (int r = 0; r < 16; ++r) xcur[i][k][r] = mv[i][k][r] + xcur[i][k][r];
-  }
-  if (div && p.mrf_rcp != 0.f) {
+        for (int i = 0; i < WM; ++i)
 #pragma unroll
-    for (int i = 0; i < WM; ++i)
+          for (int k = 0; k < WN; ++k)
 #pragma unroll
-      for (int k = 0; k < WN; ++k)
+            for (int r = 0; r < 16; ++r) xcur[i][k][r] = xcur[i][k][r] + acc[i][k][r];
+        if (cv + 2 < n_conv) {
+          write_operand(xcur, 1.0f);
+          lds_barrier();
+        }
+      }
+    } else {
+      for (int cv = 0; cv < n_conv; cv += 2) {
+        run_conv(cv);
+        stamp(3 + 2 * cv);
+        finalize(cv);
+        if (cv > 0) radius += (KT - 1) / 2 * p.dil[cv];  // conv 0: exact (margins from x)
+        wave_amax(acc, radius);
+        lds_barrier();  // every wave is done reading the operand; the maxima are posted
+        ex = block_exp();
+        write_operand(acc, exp2i(ex));
+        lds_barrier();
+        stamp(4 + 2 * cv);
+        run_conv(cv + 1);
+        stamp(5 + 2 * cv);
+        finalize(cv + 1);
+        radius += (KT - 1) / 2;  // conv2: dilation 1
 #pragma unroll
-        for (int r = 0; r < 16; ++r) xcur[i][k][r] = div_fast(xcur[i][k][r], p.mrf_div, p.mrf_rcp);
-  } else if (div) {
+        for (int i = 0; i < WM; ++i)
 #pragma unroll
-    for (int i = 0; i < WM; ++i)
+          for (int k = 0; k < WN; ++k)
 #pragma unroll
-      for (int k = 0; k < WN; ++k)
+            for (int r = 0; r < 16; ++r) xcur[i][k][r] = xcur[i][k][r] + acc[i][k][r];
+        if (cv + 2 < n_conv) {
+          wave_amax(xcur, radius);
+          lds_barrier();
+          ex = block_exp();
+          write_operand(xcur, exp2i(ex));
+          lds_barrier();
+        }
+        stamp(6 + 2 * cv);
+      }
+    }
+
+    // ---- the next window of a persistent block (block-uniform) ----
+    int wn = w + wstride;
+    if constexpr (PERSIST)
+      while (wn < n_win && !valid(wn)) wn += wstride;
+    const bool more = PERSIST && wn < n_win;
+
+    // ---- MRF: (mrf + x) [/ n_res] on the window centre ----
+    const __amdgpu_buffer_rsrc_t mrs = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(p.mrf + (int64_t)b * p.bs), 0, (int)0xFFFFFFFFu, 0x00020000);
+    bool ok[WN];
+    unsigned vo[WN];
 #pragma unroll
-        for (int r = 0; r < 16; ++r) xcur[i][k][r] = xcur[i][k][r] / p.mrf_div;
-  }
-#pragma unroll
-  for (int i = 0; i < WM; ++i)
-#pragma unroll
-    for (int k = 0; k < WN; ++k)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) asm volatile("" ::"v"(xcur[i][k][r]));
-  if constexpr (C == 32) {
-    if (post) conv_post_tail<NT, NWIN, WN>(p, xcur, ok, lds, b, len_b, t0, tid, cbase, half, col);
-  }
-#pragma unroll
-  for (int k = 0; k < WN; ++k) {
-    if (ok[k] && !post) {
+    for (int k = 0; k < WN; ++k) {
+      const int c = cbase + 32 * k + col;
+      ok[k] = vk[k] && c >= c_lo && c < c_hi;
+      vo[k] = ok[k] ? (lrow + (unsigned)(ws + c)) * 4u : 0u;
+    }
+    const bool skip_mrf = kAblate && (dbg & 16);  // ablation: no MRF epilogue
+    // persistent grid: the next window's x copy is issued first, then the MRF loads, so the
+    // two round trips overlap (one wait for both)
+    int bn = b, len_n = len_b, wsn = ws;
+    if (more) {
+      bn = item_of(wn);
+      len_n = len_of(bn);
+      wsn = (wn - bn * n_tiles) * p.W - p.halo;
+      lds_barrier();  // every wave is done reading the last conv's operand
+      dma_x(wsn, bn);
+    }
+    // every MRF load is issued before any use (one wait for all 16 x WN), then the adds /
+    // divisions for every tile; the empty asm keeps the compiler from sinking a tile's loads
+    // into its store branch (which serialised one HBM round trip per element)
+    // (the MRF values land in the accumulator registers, dead after the last conv: the
+    // persistent variant has no VGPRs to spare for a separate set)
+    floatx16 (&mv)[WM][WN] = acc;
+    if (add && !skip_mrf) {
 #pragma unroll
       for (int i = 0; i < WM; ++i)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          // through a scalar: __builtin_bit_cast of an ext_vector element lvalue compiled to
-          // element 0 of the vector (every row stored the same value)
-          const float v = xcur[i][k][r];
-          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), mrs, (int)vo[k], (int)srow(i, r), 0);
-        }
+        for (int k = 0; k < WN; ++k)
+#pragma unroll
+          for (int r = 0; r < 16; ++r)
+            mv[i][k][r] = __builtin_bit_cast(
+                float, __builtin_amdgcn_raw_buffer_load_b32(mrs, (int)vo[k], (int)srow(i, r), 0));
     }
+    if (more) wait_vm<0>();  // the x copy (and the MRF values) have landed
+    if (add && !skip_mrf) {
+#if HFG_RB_TIMING
+      wait_vm<0>();
+      stamp(23);
+#endif
+#pragma unroll
+      for (int i = 0; i < WM; ++i)
+#pragma unroll
+        for (int k = 0; k < WN; ++k)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) xcur[i][k][r] = mv[i][k][r] + xcur[i][k][r];
+    }
+    if (!skip_mrf) {
+      if (div && p.mrf_rcp != 0.f) {
+#pragma unroll
+        for (int i = 0; i < WM; ++i)
+#pragma unroll
+          for (int k = 0; k < WN; ++k)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) xcur[i][k][r] = div_fast(xcur[i][k][r], p.mrf_div, p.mrf_rcp);
+      } else if (div) {
+#pragma unroll
+        for (int i = 0; i < WM; ++i)
+#pragma unroll
+          for (int k = 0; k < WN; ++k)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) xcur[i][k][r] = xcur[i][k][r] / p.mrf_div;
+      }
+#pragma unroll
+      for (int i = 0; i < WM; ++i)
+#pragma unroll
+        for (int k = 0; k < WN; ++k)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) asm volatile("" ::"v"(xcur[i][k][r]));
+      if constexpr (C == 32) {
+        if (post) conv_post_tail<NT, NWIN, WN>(p, xcur, ok, lds, b, len_b, t0, tid, cbase, half, col);
+      }
+#pragma unroll
+      for (int k = 0; k < WN; ++k) {
+        if (ok[k] && !post) {
+#pragma unroll
+          for (int i = 0; i < WM; ++i)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+              // through a scalar: __builtin_bit_cast of an ext_vector element lvalue compiled to
+              // element 0 of the vector (every row stored the same value)
+              const float v = xcur[i][k][r];
+              __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), mrs, (int)vo[k], (int)srow(i, r), 0);
+            }
+        }
+      }
+      stamp(3 + 2 * n_conv);
+      if (p.amax_out) {  // f16x3 consumers of the stage output (block-uniform branch)
+        float m = 0.f;
+#pragma unroll
+        for (int k = 0; k < WN; ++k) {
+          float mk = 0.f;
+#pragma unroll
+          for (int i = 0; i < WM; ++i)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) mk = fmaxf(mk, fabsf(xcur[i][k][r]));
+          m = ok[k] ? fmaxf(m, mk) : m;
+        }
+        amax_commit(m, p.amax_out, b);
+      }
+    } else if (xcur[0][0][0] == 1.2345e-30f) {
+      p.mrf[0] = xcur[WM - 1][WN - 1][15];
+    }
+    if (!more) break;
+    // ---- advance: the next window's x becomes the residual stream ----
+    w = wn;
+    b = bn;
+    len_b = len_n;
+    ws = wsn;
+    t0 = ws + p.halo;
+    set_vk();
+    load_a(0, Q0);
+    load_a(1, Q0 + 1);
+    lds_barrier();  // every wave's x pieces are in LDS (each waited for its own above)
   }
-  stamp(3 + 2 * n_conv);
 #if HFG_RB_TIMING
   if (tid == 0) {
     tsv[4 + 2 * n_conv] = __builtin_amdgcn_s_memrealtime();
     for (int i = 0; i < kRbTsSlots; ++i) ts[i] = tsv[i];
   }
 #endif
-  if (p.amax_out) {  // f16x3 consumers of the stage output (block-uniform branch)
-    float m = 0.f;
-#pragma unroll
-    for (int k = 0; k < WN; ++k) {
-      float mk = 0.f;
-#pragma unroll
-      for (int i = 0; i < WM; ++i)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) mk = fmaxf(mk, fabsf(xcur[i][k][r]));
-      m = ok[k] ? fmaxf(m, mk) : m;
-    }
-    amax_commit(m, p.amax_out, b);
-  }
 }
 
 namespace {
@@ -632,36 +775,50 @@ typedef void (*RbFn)(const RbParams);
 
 struct EntryRb {
   int kt, waves_m, waves_n, wm, np, fmt;
+  bool persist;
   RbFn fn;
   char name[64];
   int C() const { return 32 * wm * waves_m; }
   int nwin() const { return 32 * (4 / wm) * waves_n; }
 };
 
-#define HFGRB_ENTRY(KT, WMS, WNS, WM, NP, FMT) \
-  { KT, WMS, WNS, WM, NP, FMT, resblock_bf16x3<KT, WMS, WNS, WM, NP, FMT>, {0} }
-#define HFGRB_KTS(WMS, WNS, WM, NP, FMT)                                                   \
-  HFGRB_ENTRY(3, WMS, WNS, WM, NP, FMT), HFGRB_ENTRY(5, WMS, WNS, WM, NP, FMT),            \
-      HFGRB_ENTRY(7, WMS, WNS, WM, NP, FMT), HFGRB_ENTRY(11, WMS, WNS, WM, NP, FMT)
+#define HFGRB_ENTRY(KT, WMS, WNS, WM, NP, FMT, PS) \
+  { KT, WMS, WNS, WM, NP, FMT, PS, resblock_bf16x3<KT, WMS, WNS, WM, NP, FMT, PS>, {0} }
+#define HFGRB_KTS(WMS, WNS, WM, NP, FMT, PS)                                                 \
+  HFGRB_ENTRY(3, WMS, WNS, WM, NP, FMT, PS), HFGRB_ENTRY(5, WMS, WNS, WM, NP, FMT, PS),      \
+      HFGRB_ENTRY(7, WMS, WNS, WM, NP, FMT, PS), HFGRB_ENTRY(11, WMS, WNS, WM, NP, FMT, PS)
 // 32-row waves (WM 1): C = 64 (2 x 4 waves), C = 32 (1 x 4), C = 128 (4 x 2, k = 3),
 // C = 64 narrow (2 x 2, k = 3).  64-row waves (WM 2: half the LDS operand reads per MFMA,
 // twice the weight-fragment loads) measured the same in a same-box A/B (round 4) and are not
 // instantiated.
-#define HFGRB_SET(NP, FMT)                                                                 \
-  HFGRB_KTS(2, 4, 1, NP, FMT), HFGRB_KTS(1, 4, 1, NP, FMT), HFGRB_ENTRY(3, 4, 2, 1, NP, FMT), \
-      HFGRB_ENTRY(3, 2, 2, 1, NP, FMT)
+// Persistent variants (PERSIST: a grid of resident blocks walks the windows, each window's
+// x copied to LDS beside the previous window's MRF round trip) for C = 64 with the
+// 512-column window (one block per CU).  Measured and not built: C = 128 (+0.9 %) and
+// C = 32 (two blocks per CU: +2 to +5 %), profiles/r05/ab.
+#define HFGRB_SET(NP, FMT)                                                                   \
+  HFGRB_KTS(2, 4, 1, NP, FMT, false), HFGRB_KTS(1, 4, 1, NP, FMT, false),                     \
+      HFGRB_ENTRY(3, 4, 2, 1, NP, FMT, false), HFGRB_ENTRY(3, 2, 2, 1, NP, FMT, false),        \
+      HFGRB_KTS(2, 4, 1, NP, FMT, true)
 
 // bf16x3 (NP 3, bf16), f16x3 (NP 3, f16), bf16w (NP 2 on the f16 kernels)
 EntryRb g_entriesRb[] = {HFGRB_SET(3, 0), HFGRB_SET(3, 1), HFGRB_SET(2, 1)};
 
-EntryRb* find_rb(int C, int nwin, int wm, int kt, int np, int fmt) {
+EntryRb* find_rb(int C, int nwin, int wm, int kt, int np, int fmt, bool persist = false) {
   for (auto& e : g_entriesRb)
-    if (e.kt == kt && e.C() == C && e.nwin() == nwin && e.wm == wm && e.np == np && e.fmt == fmt)
+    if (e.kt == kt && e.C() == C && e.nwin() == nwin && e.wm == wm && e.np == np && e.fmt == fmt &&
+        e.persist == persist)
       return &e;
   return nullptr;
 }
 
 }  // namespace
+
+__global__ void spin_kernel(int us) { stagger_wait(us); }
+
+hipError_t launch_spin(int us, hipStream_t stream) {
+  spin_kernel<<<1, 64, 0, stream>>>(us);
+  return hipGetLastError();
+}
 
 bool rb_supported(int C, int kt, int nwin, int wm) {
   return find_rb(C, nwin, wm, kt, 3, 0) != nullptr;
@@ -674,23 +831,31 @@ size_t rb_lds_bytes(int C, int nwin, int n_conv) {
 }
 
 hipError_t launch_resblock_bf16x3(int C, int nwin, int wm, int kt, int fmt, int np,
-                                  const RbParams& p, int batch, hipStream_t stream,
+                                  const RbParams& p_in, int batch, hipStream_t stream,
                                   const char** name) {
-  EntryRb* e = find_rb(C, nwin, wm, kt, np, fmt);
+  RbParams p = p_in;
+  p.batch = batch;
+  // a persistent variant where one is built (one-block-per-CU shapes), else one window per block
+  EntryRb* e = p.persist ? find_rb(C, nwin, wm, kt, np, fmt, true) : nullptr;
+  if (!e) {
+    p.persist = 0;
+    e = find_rb(C, nwin, wm, kt, np, fmt);
+  }
   if (!e) return hipErrorInvalidValue;
   if (p.n_conv < 2 || p.n_conv > kRbMaxConv || (p.n_conv & 1)) return hipErrorInvalidValue;
   if (p.conv0 < 0 || p.conv0 + p.n_conv > p.n_conv_stream) return hipErrorInvalidValue;
   if (p.W <= 0 || p.halo < 0 || p.W + 2 * p.halo > nwin) return hipErrorInvalidValue;
   if (p.wav && (C != 32 || wm != 1 || p.L % 4 || p.W % 4 || p.halo < 4 || !p.post_w || !p.post_b ||
-                p.amax_out))
+                p.amax_out || p.persist))
     return hipErrorInvalidValue;
+  if (p.persist < 0 || batch < 1) return hipErrorInvalidValue;
   for (int i = 0; i < p.n_conv; ++i)
     if (p.dil[i] < 1 || (kt - 1) / 2 * p.dil[i] > rb_marg(C, nwin)) return hipErrorInvalidValue;
   {
     std::lock_guard<std::mutex> lk(setup_mutex());
     if (!e->name[0])
-      snprintf(e->name, sizeof(e->name), "resblock_bf16x3<%d, %d, %d, %d, %d, %d>", e->kt,
-               e->waves_m, e->waves_n, e->wm, e->np, e->fmt);
+      snprintf(e->name, sizeof(e->name), "resblock_bf16x3<%d, %d, %d, %d, %d, %d%s>", e->kt,
+               e->waves_m, e->waves_n, e->wm, e->np, e->fmt, e->persist ? ", persist" : "");
   }
 #if HFG_RB_TIMING
   const size_t lds = rb_lds_bytes(C, nwin, p.n_conv) + kRbTsSlots * 8;  // + the stamps
@@ -702,7 +867,14 @@ hipError_t launch_resblock_bf16x3(int C, int nwin, int wm, int kt, int fmt, int 
     return err;
   if (name) *name = e->name;
   const int n_tiles = (p.L + p.W - 1) / p.W;
-  e->fn<<<dim3(n_tiles, batch), dim3(64 * e->waves_m * e->waves_n), lds, stream>>>(p);
+  if (p.persist) {
+    const int64_t n_win = (int64_t)n_tiles * batch;
+    if (n_win >= (1ll << 31)) return hipErrorInvalidValue;
+    const int g = (int)std::min<int64_t>(n_win, p.persist);
+    e->fn<<<dim3(g, 1), dim3(64 * e->waves_m * e->waves_n), lds, stream>>>(p);
+  } else {
+    e->fn<<<dim3(n_tiles, batch), dim3(64 * e->waves_m * e->waves_n), lds, stream>>>(p);
+  }
   return hipGetLastError();
 }
 
