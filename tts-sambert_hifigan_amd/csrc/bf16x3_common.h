@@ -151,12 +151,6 @@ __device__ __forceinline__ float div_fast(float x, float d, float rcp) {
   return __builtin_amdgcn_classf(q0, 0x264) ? q0 : q;
 }
 
-// block stagger (experiment): spin ~us microseconds on the 100-MHz real-time counter
-__device__ __forceinline__ void stagger_wait(int us) {
-  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-  while (__builtin_amdgcn_s_memrealtime() - t0 < (uint64_t)us * 100u) __builtin_amdgcn_s_sleep(8);
-}
-
 // s_waitcnt vmcnt(N) with a compile-time N
 template <int N>
 __device__ __forceinline__ void wait_vm() {

@@ -133,11 +133,6 @@ conv1d_bf16x3(const ConvParams p) {
     tx = __builtin_amdgcn_readfirstlane(tx);
     b = __builtin_amdgcn_readfirstlane(b);
   }
-  if (AREG && p.stag_n > 0) {  // block-uniform: SALU only
-    const int id = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
-    if (id >= p.stag_lo && id < p.stag_hi)
-      stagger_wait(p.stag_n);
-  }
   const int n0 = p.n_base + tx * NTILE;
   const int half = lane >> 5;
   const int col = lane & 31;

@@ -4,7 +4,6 @@
 // management and the 78-launch forward schedule of
 // HiFiGANGenerator.forward (models/hifigan.py:224-261).
 #include <hip/hip_runtime.h>
-#include <hip/hip_ext.h>
 
 #include <algorithm>
 #include <cmath>
@@ -183,17 +182,10 @@ struct hfg_handle {
   int small_tile = -1;       // small-grid tile: -1 auto (grid < kSmallGridBlocks), 0 never,
                              // 1 always (HFG_SMALL_TILE; bitwise invisible)
   int dbg_flags = 0;  // HFG_DEBUG_FLAGS (kernel ablations, -DHFG_ABLATE=1 builds only)
-  // HFG_STAGGER="conv,rb": microseconds the first round's second-half blocks in the
-  // multi-round tile-5 layer-conv and whole-ResBlock grids wait (experiment; 0 = off)
-  int stag_conv = 0, stag_rb = 0;
   // HFG_RB_PERSIST (default 2): persistent grids for the one-block-per-CU ResBlock launches
   int rb_persist = 2;
   int n_cu = 256;      // compute units of the device (hipDeviceAttributeMultiprocessorCount)
   int halves = 1;      // batch halves of the running forward (2: two streams share the CUs)
-  // HFG_CU_SPLIT="1[,delay_us]" (experiment): the two batch halves on streams masked to
-  // disjoint halves of the CUs, the second half started delay_us later
-  int cu_split = 0, cu_delay = 0;
-  hipStream_t cu_s[2] = {nullptr, nullptr};
   // batch split over two HIP streams (HFG_SPLIT=1 disables): the two halves' launches
   // overlap, so one half's ramp-down / epilogue tail runs beside the other's main loops
   int split = 2;
@@ -1110,11 +1102,6 @@ int run_conv(hfg_handle* h, Launcher& ln, const Layer& L, const float* x, int64_
   const int ntile = L.prec == 1 ? hfg::kBf16x3Tiles[L.tile].NTILE() : kTiles[L.tile].NTILE();
   int n_tiles = (int)((Lt + ntile - 1) / ntile), m_tiles = L.m_tiles;
   const int tile = pick_tile(h, L, p, Lt, B, ln.conc, n_tiles, m_tiles);
-  if (h->stag_conv > 0 && hfg::kBf16x3Tiles[tile].AREG && (int64_t)n_tiles * m_tiles * B >= 1024) {
-    p.stag_lo = 256;
-    p.stag_hi = 512;
-    p.stag_n = h->stag_conv;
-  }
   const double flop = 2.0 * L.C_out * L.C_in * L.k * (double)Lt * B;
   double bytes = 4.0 * B * Lt * (L.C_in + L.C_out) + 4.0 * L.C_out * L.C_in * L.k;
   if (res) bytes += 4.0 * B * Lt * L.C_out;
@@ -1187,14 +1174,6 @@ int run_resblock(hfg_handle* h, Launcher& ln, const RbFused& rb, const float* x,
     // of the half-batch stream's share (n_CU / halves), 2 one per CU
     if (h->rb_persist && per_cu == 1 && !(last && post))
       p.persist = std::max(1, h->n_cu / (h->rb_persist == 1 ? h->halves : 1));
-    if (h->stag_rb > 0) {
-      const int64_t blocks = (Lt + p.W - 1) / p.W * B;
-      if (blocks >= 2 * 256 * per_cu) {
-        p.stag_lo = 128 * per_cu;
-        p.stag_hi = 256 * per_cu;
-        p.stag_n = h->stag_rb;
-      }
-    }
     double bytes =
         4.0 * B * Lt * C * ((last && (mrf_mode & 1)) ? 3 : 2) + 4.0 * (double)rb.w_len;
     if (last && post) {
@@ -1665,34 +1644,11 @@ int forward_split(hfg_handle* h, const float* mel, int64_t B, int64_t T,
   const int64_t B1 = (B + 1) / 2, B2 = B - B1;
   const size_t w1 = ws_part_bytes(h, B1, T);
   hipStream_t s0 = stream, s1 = h->aux;
-  if (h->cu_split && h->device >= 0) {
-    if (!h->cu_s[0]) {
-      const int nw = (h->n_cu + 31) / 32;
-      for (int k = 0; k < 2; ++k) {
-        std::vector<uint32_t> mask(nw, 0u);
-        for (int c = k * h->n_cu / 2; c < (k + 1) * h->n_cu / 2; ++c) mask[c / 32] |= 1u << (c % 32);
-        hipError_t e = hipExtStreamCreateWithCUMask(&h->cu_s[k], (uint32_t)nw, mask.data());
-        if (e != hipSuccess) return hip_fail(e, "create CU-masked stream");
-      }
-    }
-    s0 = h->cu_s[0];
-    s1 = h->cu_s[1];
-  }
   hipError_t e = hipEventRecord(h->fork_ev, stream);
   if (e == hipSuccess) e = hipStreamWaitEvent(s1, h->fork_ev, 0);
-  if (e == hipSuccess && s0 != stream) e = hipStreamWaitEvent(s0, h->fork_ev, 0);
   if (e != hipSuccess) return hip_fail(e, "fork");
-  if (h->cu_split && h->cu_delay > 0) {
-    e = hfg::launch_spin(h->cu_delay, s1);
-    if (e != hipSuccess) return hip_fail(e, "spin");
-  }
   int rc = forward_impl(h, mel, B1, T, o, wav, out_len, ws, w1, s0, 0);
   if (rc) return rc;
-  if (s0 != stream) {
-    e = hipEventRecord(h->fork_ev, s0);
-    if (e == hipSuccess) e = hipStreamWaitEvent(stream, h->fork_ev, 0);
-    if (e != hipSuccess) return hip_fail(e, "join");
-  }
   hfg_forward_opts o2{};
   if (o) {
     o2 = *o;
@@ -1726,9 +1682,7 @@ int create_impl(const hfg_config* cfg, bool mrf_only, int device, hfg_handle** o
 #if HFG_ABLATE
   if (const char* dbg = getenv("HFG_DEBUG_FLAGS")) h->dbg_flags = atoi(dbg);
 #endif
-  if (const char* sg = getenv("HFG_STAGGER")) sscanf(sg, "%d,%d", &h->stag_conv, &h->stag_rb);
   if (const char* rp = getenv("HFG_RB_PERSIST")) h->rb_persist = std::min(2, std::max(0, atoi(rp)));
-  if (const char* cs = getenv("HFG_CU_SPLIT")) sscanf(cs, "%d,%d", &h->cu_split, &h->cu_delay);
   if (device >= 0) {
     int n = 0;
     if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess &&
@@ -1839,8 +1793,6 @@ void hfg_destroy(hfg_handle* h) {
       if (h->fork_ev) (void)hipEventDestroy(h->fork_ev);
       if (h->join_ev) (void)hipEventDestroy(h->join_ev);
       if (h->aux) (void)hipStreamDestroy(h->aux);
-      for (auto& cs : h->cu_s)
-        if (cs) (void)hipStreamDestroy(cs);
       for (int part = 0; part < 2; ++part) {
         if (h->rb_fork[part]) (void)hipEventDestroy(h->rb_fork[part]);
         for (int j = 0; j < HFG_MAX_RES; ++j) {

@@ -62,10 +62,6 @@ struct ConvParams {
   const uint32_t* amax_in;
   uint32_t* amax_out;
   int ew;
-  // block stagger (tile 5): blocks of linear id in [stag_lo, stag_hi) first wait stag_n
-  // microseconds, so the co-resident blocks of a multi-round grid do not run
-  // their epilogues in lockstep (0: off)
-  int stag_lo, stag_hi, stag_n;
   int dbg;           // ablation flags (HFG_DEBUG_FLAGS, builds with -DHFG_ABLATE=1 only; wrong
                      // results when set), bf16x3 kernel: bit0 skip input restaging after the
                      // first chunk, bit2 no per-chunk barrier, bit3 no epilogue, bit7 every
@@ -264,7 +260,6 @@ struct RbParams {
   const float* post_w;   // conv_post weight [C][7] fp32
   const float* post_b;   // conv_post bias [1]
   float* wav;
-  int stag_lo, stag_hi, stag_n;  // block stagger (ConvParams)
   int batch;             // items (set by launch_resblock_bf16x3)
   // persistent grid (one-block-per-CU instances; not with the fused conv_post): 0 = one window
   // per block, else the launch runs min(windows, persist) blocks that walk the windows and
@@ -278,8 +273,6 @@ struct RbParams {
 inline bool fast_div_ok(float d) {
   return d == 1.f || d == 2.f || d == 3.f || d == 4.f || d == 5.f || d == 7.f || d == 8.f;
 }
-// one wave spinning `us` microseconds on `stream` (schedule experiments: a delayed stream)
-hipError_t launch_spin(int us, hipStream_t stream);
 bool rb_supported(int C, int kt, int nwin, int wm);
 size_t rb_lds_bytes(int C, int nwin, int n_conv);
 hipError_t launch_resblock_bf16x3(int C, int nwin, int wm, int kt, int fmt, int np,

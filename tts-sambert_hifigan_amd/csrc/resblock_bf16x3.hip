@@ -168,11 +168,6 @@ resblock_bf16x3(const RbParams p) {
     w += wstride;
   }
   if (w >= n_win) return;
-  if (p.stag_n > 0) {
-    const int id = blockIdx.x + gridDim.x * blockIdx.y;
-    if (id >= p.stag_lo && id < p.stag_hi)
-      stagger_wait(p.stag_n);
-  }
   int b = item_of(w);
   int len_b = len_of(b);
   int t0 = (w - b * n_tiles) * p.W;
@@ -812,13 +807,6 @@ EntryRb* find_rb(int C, int nwin, int wm, int kt, int np, int fmt, bool persist 
 }
 
 }  // namespace
-
-__global__ void spin_kernel(int us) { stagger_wait(us); }
-
-hipError_t launch_spin(int us, hipStream_t stream) {
-  spin_kernel<<<1, 64, 0, stream>>>(us);
-  return hipGetLastError();
-}
 
 bool rb_supported(int C, int kt, int nwin, int wm) {
   return find_rb(C, nwin, wm, kt, 3, 0) != nullptr;
