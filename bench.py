@@ -139,6 +139,10 @@ def parse():
                     help="HIP streams per forward (hfg_set_streams): 2 = batch halves overlap "
                          "(production default); per-kernel roofline figures always come from "
                          "a 1-stream profiled pass")
+    ap.add_argument("--graph", action="store_true",
+                    help="time the value pass as replays of one captured hipGraph of the forward "
+                         "(both streams: fork / join events are captured); the per-kernel pass "
+                         "stays eager")
     ap.add_argument("--no-profile", action="store_true",
                     help="do not bracket launches with HIP events (no roofline)")
     ap.add_argument("--no-pmc", action="store_true",
@@ -539,6 +543,27 @@ def main():
         for _ in range(args.warmup):
             step()
         torch.cuda.synchronize(dev)
+        eager_step = step
+        if args.graph:
+            # one forward captured on a side stream, replayed on `stream` (the handle forks its
+            # second half onto its internal stream with events, which the capture records)
+            side = torch.cuda.Stream(dev)
+            side.wait_stream(stream)
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.stream(side):
+                with torch.cuda.graph(graph, stream=side):
+                    h.forward_ws(mel.data_ptr(), B, T, wav.data_ptr(), out_len, ws.data_ptr(),
+                                 ws_bytes, side.cuda_stream)
+            stream.wait_stream(side)
+            torch.cuda.synchronize(dev)
+
+            def step():
+                with torch.cuda.stream(stream):
+                    graph.replay()
+
+            for _ in range(args.warmup):
+                step()
+            torch.cuda.synchronize(dev)
         profile = not args.no_profile
         # with 2 streams the timed loop runs uninstrumented (its per-launch intervals would
         # overlap anyway); the per-kernel events come from the 1-stream pass below
@@ -579,20 +604,20 @@ def main():
                 # K steps again on one stream, every launch bracketed by HIP events on it
                 h.set_streams(1)
                 for _ in range(args.warmup):
-                    step()
+                    eager_step()
                 torch.cuda.synchronize(dev)
                 h.profile_reset()
                 h.set_profiling(True)
                 t1 = time.perf_counter()
                 for _ in range(args.steps):
-                    step()
+                    eager_step()
                 torch.cuda.synchronize(dev)
                 prof_ms[precision] = 1000.0 * (time.perf_counter() - t1) / args.steps
                 h.set_profiling(False)
                 prof = h.profile_summary()
                 h.set_streams(args.streams)
         if precision == args.precision and not args.pmc_child:
-            e2e[precision] = end_to_end(step, wav)
+            e2e[precision] = end_to_end(eager_step, wav)
         del ws, wav
         return elapsed, prof, out_len
 
@@ -679,6 +704,9 @@ def main():
                    else "external launcher" if "RANK" in os.environ else "single process"),
         "value_note": "value = whole-job aggregate (all ranks' samples / max-over-ranks time, the "
                       "bench contract); value_per_gpu = value / n_gpus",
+        "value_pass": ("hipGraph replays of one captured forward" if args.graph
+                       else "eager forwards (hfg_forward_ws per step)") +
+                      f", {args.streams} stream(s)",
         "rtf": (elapsed / args.steps) / (args.batch * out_len / SAMPLE_RATE),
         "step_ms_hipevent_median": ev_median.get(args.precision),
         "samples_per_s_hipevent_median": (args.batch * out_len / (ev_median[args.precision] * 1e-3)

@@ -34,6 +34,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <type_traits>
 #include <mutex>
 
 #include <cstdio>
@@ -62,9 +63,10 @@ typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 // conv_post + tanh (models/hifigan.py:254-256) fused into the network's last MRF write (C = 32,
 // one 32-row wave per window slice): the exact final x on the window columns [halo - 3,
 // halo + W + 3) is staged as lrelu(x) in LDS ([channel][column + sh] fp32, 0 outside those
-// columns and outside [0, len)), then one thread per 4 consecutive samples sums over
-// (channel, tap) in conv_post4_tanh's order (channel-major, fma from 0, bias last): bitwise the
-// separate kernel's wav, without the stage output's HBM write and read.
+// columns and outside [0, len)), then one thread per 2 consecutive samples (each quad split over
+// the two halves of the block) sums over (channel, tap) in conv_post4_tanh's order (channel-
+// major, fma from 0, bias last): bitwise the separate kernel's wav, without the stage output's
+// HBM write and read.
 template <int NT, int NWIN, int WN>
 __device__ __forceinline__ void conv_post_tail(const RbParams& p, const floatx16 (&xcur)[1][WN],
                                                const bool (&ok)[WN], char* lds, int b, int len_b,
@@ -86,30 +88,41 @@ __device__ __forceinline__ void conv_post_tail(const RbParams& p, const floatx16
   lds_barrier();
   const float bias = p.post_b[0];
   float* const wav = p.wav + (int64_t)b * p.L;
-  for (int q = tid; q < p.W / 4; q += NT) {
-    const int t = t0 + 4 * q;  // p.L % 4 == 0 (host): a quad is wholly inside or past the row
-    if (t >= p.L) break;
-    // element k of v = column t - 4 + k (conv_post4_tanh's layout)
-    const float* xs = s + p.halo + sh + 4 * q - 4;
-    float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  // the first half of the threads computes samples 0, 1 of each quad, the second half samples
+  // 2, 3 (wave-uniform: two specialised code paths), so every wave works on the tail
+  static_assert(NT % 128 == 0, "whole waves per half");
+  const int hq = __builtin_amdgcn_readfirstlane(tid / (NT / 2));
+  auto run = [&](auto h_tag) {
+    constexpr int H = decltype(h_tag)::value;
+    for (int q = tid - H * (NT / 2); q < p.W / 4; q += NT / 2) {
+      const int t = t0 + 4 * q;  // p.L % 4 == 0 (host): a quad is wholly inside or past the row
+      if (t >= p.L) break;
+      // element k of v = column t - 4 + k (conv_post4_tanh's layout)
+      const float* xs = s + p.halo + sh + 4 * q - 4;
+      float acc[2] = {0.f, 0.f};
 #pragma unroll 4
-    for (int c = 0; c < C; ++c) {
-      const f4 q0 = *reinterpret_cast<const f4*>(xs + c * S);
-      const f4 q1 = *reinterpret_cast<const f4*>(xs + c * S + 4);
-      const f4 q2 = *reinterpret_cast<const f4*>(xs + c * S + 8);
-      const float v[12] = {q0[0], q0[1], q0[2], q0[3], q1[0], q1[1],
-                           q1[2], q1[3], q2[0], q2[1], q2[2], q2[3]};
-      const float* w = p.post_w + c * KP;
+      for (int c = 0; c < C; ++c) {
+        const f4 q0 = *reinterpret_cast<const f4*>(xs + c * S);
+        const f4 q1 = *reinterpret_cast<const f4*>(xs + c * S + 4);
+        const f4 q2 = *reinterpret_cast<const f4*>(xs + c * S + 8);
+        const float v[12] = {q0[0], q0[1], q0[2], q0[3], q1[0], q1[1],
+                             q1[2], q1[3], q2[0], q2[1], q2[2], q2[3]};
+        const float* w = p.post_w + c * KP;
 #pragma unroll
-      for (int o = 0; o < 4; ++o)
+        for (int o = 0; o < 2; ++o)
 #pragma unroll
-        for (int j = 0; j < KP; ++j) acc[o] = fmaf(w[j], v[o + j + 1], acc[o]);
+          for (int j = 0; j < KP; ++j) acc[o] = fmaf(w[j], v[2 * H + o + j + 1], acc[o]);
+      }
+      floatx2 r;
+#pragma unroll
+      for (int o = 0; o < 2; ++o) r[o] = t + 2 * H + o >= len_b ? 0.f : tanhf(acc[o] + bias);
+      *reinterpret_cast<floatx2*>(wav + t + 2 * H) = r;
     }
-    f4 r;
-#pragma unroll
-    for (int o = 0; o < 4; ++o) r[o] = t + o >= len_b ? 0.f : tanhf(acc[o] + bias);
-    *reinterpret_cast<f4*>(wav + t) = r;
-  }
+  };
+  if (hq == 0)
+    run(std::integral_constant<int, 0>{});
+  else
+    run(std::integral_constant<int, 1>{});
 }
 
 template <int KT, int WAVES_M, int WAVES_N, int WM, int NP, int FMT, bool PERSIST>
