@@ -355,8 +355,12 @@ __device__ __forceinline__ void conv_epilogue_lds2(const ConvParams& p, floatx16
         const int row = row_base + i * 32 + rr, n = n_base + 4 * c4;
         const bool ok = row < p.M && n < N_b;
         const int64_t o = (int64_t)row * p.N + n;
+        // ablation bits 15 / 16 (timing only): the residual read from the tile's columns of row
+        // 0 (L2-warm after the first wave) / not read at all
+        const int64_t orr = (kAblate && (p.dbg & 32768)) ? (int64_t)n : o;
         if constexpr (R)
-          rv[j] = ok ? *reinterpret_cast<const float4*>(resb + o) : float4{0.f, 0.f, 0.f, 0.f};
+          rv[j] = ok && !(kAblate && (p.dbg & 65536)) ? *reinterpret_cast<const float4*>(resb + orr)
+                                                      : float4{0.f, 0.f, 0.f, 0.f};
         if constexpr (M)
           mv[j] = ok ? *reinterpret_cast<const float4*>(outb + o) : float4{0.f, 0.f, 0.f, 0.f};
       });
