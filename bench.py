@@ -694,7 +694,9 @@ def main():
             "batch_per_gpu": args.batch,
             "frames": T,
             "global_batch": global_batch,
-            "parallelism": f"dp{world} (utterance-sharded, RCCL weight broadcast at init)",
+            "parallelism": (f"dp{world} (utterance-sharded, "
+                            f"{'RCCL' if args.dist_backend == 'nccl' else 'gloo'} weight broadcast at init)"
+                            if use_dist else "dp1"),
         },
         "value_per_gpu": value / world,
         "per_rank_ms_per_step": rank_ms.get(args.precision),
