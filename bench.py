@@ -165,6 +165,22 @@ def _norm(name: str) -> str:
     return name.replace(" ", "")
 
 
+def _pmc_key(label: str, pmc: dict):
+    """The rocprofv3 name (normalised) of a library profile label, or None: the whole-ResBlock
+    labels name the persistent grid 'persist' and leave the non-persistent flag out, where the
+    kernel's own name carries its last template argument (true / false)."""
+    n = _norm(label)
+    cands = [n, n + "_kernel"]
+    if n.startswith("resblock_bf16x3<") and n.endswith(">"):
+        args_ = n[len("resblock_bf16x3<"):-1].split(",")
+        if args_[-1] == "persist":
+            args_[-1] = "true"
+        elif len(args_) == 6:
+            args_.append("false")
+        cands.append("resblock_bf16x3<" + ",".join(args_) + ">")
+    return next((c for c in cands if c in pmc), None)
+
+
 def _host_cores():
     """(threads to use, description): the CPUs this process may run on, capped by the
     cgroup CPU quota when one is set (a GPU box shows every host CPU in
@@ -821,8 +837,9 @@ def main():
             # per step (1-stream pass counts; the 2-stream value pass moves the same bytes)
             meas, missing = 0.0, []
             for k, v in prof.items():
-                if _norm(k) in pmc:
-                    meas += pmc[_norm(k)]["bytes"] * v["launches"] / args.steps
+                pk = _pmc_key(k, pmc)
+                if pk:
+                    meas += pmc[pk]["bytes"] * v["launches"] / args.steps
                 else:
                     missing.append(k)
             line["roofline_step"]["hbm_pmc"] = {
@@ -833,8 +850,8 @@ def main():
         line["kernels"] = {k: {"launches": v["launches"] // args.steps,
                                "ms_per_step": v["ms"] / args.steps,
                                "TFLOPs": v["flop"] / (v["ms"] * 1e-3) / 1e12 if v["ms"] else None,
-                           "pmc_bytes_per_launch": (pmc[_norm(k)]["bytes"]
-                                                    if pmc and _norm(k) in pmc else None),
+                           "pmc_bytes_per_launch": (pmc[_pmc_key(k, pmc)]["bytes"]
+                                                    if pmc and _pmc_key(k, pmc) else None),
                            "alg_bytes_per_launch": v["bytes"] / v["launches"]}
                            for k, v in sorted(prof.items(), key=lambda kv: -kv[1]["ms"])}
     if world == 1 and not args.no_extra:

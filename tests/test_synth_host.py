@@ -3,6 +3,7 @@ same architecture / state_dict layout as the reference (checked against the orac
 restatement of models/hifigan.py's parameter list), default-init bounds, and the
 SURVEY.md §8(d) canonical byte model."""
 import importlib
+import os
 
 import numpy as np
 import pytest
@@ -42,3 +43,23 @@ def test_canonical_byte_model(S):
     assert S.layer_streaming_bytes_per_frame(S.V1) == 5436736
     assert S.layer_streaming_bytes_per_frame(S.V2STAR) == 960832
     assert S.param_bytes(S.V1) == 4 * 13926017  # 13,926,017 params
+
+
+def test_bench_pmc_key_maps_profile_labels_to_kernel_names():
+    """bench.py joins the library's per-kernel profile labels with the rocprofv3 PMC rows by
+    kernel name: the whole-ResBlock labels ('persist' / no flag) map to the template's bool."""
+    import importlib.util
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(root, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    pmc = {"resblock_bf16x3<11,2,4,1,3,1,true>": {}, "resblock_bf16x3<3,4,2,1,3,1,false>": {},
+           "conv1d_bf16x3<11,2,2,2,2,4,2,false,3,true,1>": {}, "absmax_kernel": {}}
+    assert bench._pmc_key("resblock_bf16x3<11, 2, 4, 1, 3, 1, persist>", pmc) == \
+        "resblock_bf16x3<11,2,4,1,3,1,true>"
+    assert bench._pmc_key("resblock_bf16x3<3, 4, 2, 1, 3, 1>", pmc) == \
+        "resblock_bf16x3<3,4,2,1,3,1,false>"
+    assert bench._pmc_key("conv1d_bf16x3<11, 2, 2, 2, 2, 4, 2, false, 3, true, 1>", pmc) == \
+        "conv1d_bf16x3<11,2,2,2,2,4,2,false,3,true,1>"
+    assert bench._pmc_key("absmax", pmc) == "absmax_kernel"
+    assert bench._pmc_key("ups_bf16x3<1, 4, 1, 2, 3, 1>", pmc) is None
