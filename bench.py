@@ -134,7 +134,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extra", action="store_true",
                     help="skip the other BASELINE configs (C1 latency + hipGraph, C4 V2*, C5 ragged)")
-    ap.add_argument("--cpu-budget-s", type=float, default=12.0)
+    ap.add_argument("--cpu-budget-s", type=float, default=30.0)
     ap.add_argument("--streams", type=int, default=2, choices=[1, 2],
                     help="HIP streams per forward (hfg_set_streams): 2 = batch halves overlap "
                          "(production default); per-kernel roofline figures always come from "
@@ -261,32 +261,44 @@ def pmc_traffic(argv_extra):
         shutil.rmtree(tmp, ignore_errors=True)
 
 
-def cpu_baseline(cfg, sd, frames, budget_s):
-    """Oracle (PyTorch-CPU restatement) on host cores: best of N runs of one
-    [1, 80, frames] utterance after a warm-up, within ~budget_s seconds."""
+def cpu_baseline(cfg, sd, batch, frames, budget_s):
+    """Oracle (PyTorch-CPU restatement) on host cores, on the bench line's own workload:
+    [batch, 80, frames] (C2 = [8, 80, 1024]), best of N runs after a warm-up, as many as fit
+    in ~budget_s (at least one).  The one-utterance [1, 80, frames] rate (the
+    CPU runs batch 8 at about half its batch-1 rate) is reported beside it as `batch1`."""
     from oracle import config as OC, hifigan_torch, prng  # the CPU baseline leg only
     cfg = OC.GenConfig(**cfg.kwargs())
     threads, cores_desc = _host_cores()
     prev = torch.get_num_threads()
     torch.set_num_threads(threads)
     tsd = hifigan_torch.to_torch_state(sd)
-    mel = torch.from_numpy(prng.mel_input(1234, (1, cfg.n_mels, frames)))
-    hifigan_torch.generator_forward(tsd, cfg, mel[:, :, :32])  # warm-up
-    best, runs, t_all = None, 0, time.perf_counter()
-    while runs < 1 or (time.perf_counter() - t_all < budget_s and runs < 3):
-        t0 = time.perf_counter()
-        wav = hifigan_torch.generator_forward(tsd, cfg, mel)
-        dt = time.perf_counter() - t0
-        best = dt if best is None else min(best, dt)
-        runs += 1
+    mel = torch.from_numpy(prng.mel_input(1234, (batch, cfg.n_mels, frames)))
+
+    def best_of(x, budget):
+        best, runs, t_all = None, 0, time.perf_counter()
+        while runs < 1 or (time.perf_counter() - t_all + (best or 0.0) < budget and runs < 3):
+            t0 = time.perf_counter()
+            with torch.no_grad():
+                wav = hifigan_torch.generator_forward(tsd, cfg, x)
+            dt = time.perf_counter() - t0
+            best = dt if best is None else min(best, dt)
+            runs += 1
+        return best, runs, wav.numel()
+
+    with torch.no_grad():
+        hifigan_torch.generator_forward(tsd, cfg, mel[:1, :, :32])  # warm-up
+    best, runs, samples = best_of(mel, budget_s)
+    best1, runs1, samples1 = best_of(mel[:1], min(budget_s, 8.0))
     torch.set_num_threads(prev)
-    samples = wav.shape[-1]
     return {"value": samples / best, "unit": "audio samples/s", "cores": threads,
             "kind": "port",
-            "sample": f"1 utterance [1,{cfg.n_mels},{frames}] of the bench workload, best of {runs} "
-                      f"after warm-up, oracle/hifigan_torch.py (same ATen ops as the reference)",
+            "sample": f"the bench workload itself: [{batch},{cfg.n_mels},{frames}] -> "
+                      f"{samples} samples, best of {runs} after warm-up, oracle/hifigan_torch.py "
+                      "(same ATen ops as the reference, SURVEY.md §8(d))",
             "cores_note": cores_desc,
-            "rtf": best / (samples / SAMPLE_RATE)}
+            "rtf": best / (samples / SAMPLE_RATE),
+            "batch1": {"value": samples1 / best1, "runs": runs1,
+                       "sample": f"one utterance [1,{cfg.n_mels},{frames}], best of {runs1}"}}
 
 
 def extra_configs(pkg, S, dev, precision, steps=5):
@@ -582,8 +594,10 @@ def main():
             torch.cuda.synchronize(dev)
         profile = not args.no_profile
         # with 2 streams the timed loop runs uninstrumented (its per-launch intervals would
-        # overlap anyway); the per-kernel events come from the 1-stream pass below
-        if profile and args.streams == 1:
+        # overlap anyway), and graph replays bypass the library's launcher (no per-launch
+        # events); the per-kernel events then come from the eager 1-stream pass below
+        inline_prof = profile and args.streams == 1 and not args.graph
+        if inline_prof:
             h.profile_reset()
             h.set_profiling(True)
         evs = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
@@ -611,7 +625,7 @@ def main():
             rank_ms[precision] = [1000.0 * elapsed / args.steps]
         prof = {}
         if profile:
-            if args.streams == 1:
+            if inline_prof:
                 h.set_profiling(False)
                 prof = h.profile_summary()
             else:
@@ -632,6 +646,9 @@ def main():
                 h.set_profiling(False)
                 prof = h.profile_summary()
                 h.set_streams(args.streams)
+        # content hash of the value pass's output (hfg_checksum32): same-box A/B builds that must
+        # be bitwise equal show it (profiles/r06/lib_ab.sh)
+        wav_sum[precision] = int(pkg._lib.checksum32([wav])[0]) & 0xffffffff
         if precision == args.precision and not args.pmc_child:
             e2e[precision] = end_to_end(eager_step, wav)
         del ws, wav
@@ -663,6 +680,7 @@ def main():
     prof_ms = {}  # ms/step of the 1-stream roofline pass, per precision
     rank_ms = {}  # per-rank ms/step of the value pass, per precision
     ev_median = {}  # per-step HIP-event median (ms) of the value pass, per precision
+    wav_sum = {}  # hfg_checksum32 of the value pass's wav, per precision
     e2e = {}
     def progress(msg):
         """one stderr line per phase (a long run then shows it is alive)"""
@@ -727,6 +745,7 @@ def main():
                       f", {args.streams} stream(s)",
         "rtf": (elapsed / args.steps) / (args.batch * out_len / SAMPLE_RATE),
         "step_ms_hipevent_median": ev_median.get(args.precision),
+        "wav_checksum32": f"{wav_sum[args.precision]:08x}" if args.precision in wav_sum else None,
         "samples_per_s_hipevent_median": (args.batch * out_len / (ev_median[args.precision] * 1e-3)
                                           if ev_median.get(args.precision) else None),
     }
@@ -747,6 +766,7 @@ def main():
         for prec, (el, pr, ol) in alt.items():
             v = global_batch * ol * args.steps / el
             entry = {"value": v, "ms_per_step": 1000.0 * el / args.steps,
+                     "wav_checksum32": f"{wav_sum[prec]:08x}" if prec in wav_sum else None,
                      "rtf": (el / args.steps) / (args.batch * ol / SAMPLE_RATE),
                      "speedup_vs_headline": v / value,
                      "parity": ("atol 1e-4 vs the oracle run on the bf16-rounded weights "
@@ -859,7 +879,7 @@ def main():
     if world == 1 and not args.no_cpu_baseline:
         cfg_np = S.random_state_dict(cfg, seed=0) if sd_np is None else sd_np
         progress("CPU baseline")
-        line["cpu_baseline"] = cpu_baseline(cfg, cfg_np, T, args.cpu_budget_s)
+        line["cpu_baseline"] = cpu_baseline(cfg, cfg_np, B, T, args.cpu_budget_s)
         line["cpu_baseline"]["gpu_over_cpu"] = value / line["cpu_baseline"]["value"]
     print(json.dumps(line), flush=True)
     if use_dist:

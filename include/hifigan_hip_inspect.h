@@ -48,6 +48,18 @@ int hfg_forward_taps(hfg_handle* h, const float* mel, int64_t B, int64_t T, floa
                      int64_t out_len, void* workspace, size_t workspace_bytes,
                      float* const* taps, int n_taps, void* stream);
 
+/* Schedule overrides for A/B runs and the parity suites (process-wide; read by every
+ * later hfg_create / hfg_mrf_create / hfg_mel_create).  The library reads no environment
+ * variable for its schedule (the HFG_* knobs of rounds 1-5 are only warned about), so a
+ * production handle runs the default schedule whatever its process inherits.  Knobs:
+ * FUSED_RB 0|1, FUSE_POST 0|1, RB_SPLIT 0|1, SMALL_TILE -1|0|1, RB_CONC -1|0|1,
+ * UPS_FRAMES 1|2, SPLIT 1|2, RB_PERSIST 0..2, DEBUG_FLAGS (ablation builds), MEL_DFT 0|1.
+ * set: HFG_EINVAL for an unknown knob or a value out of range.  clear: one knob, or all
+ * with knob == NULL.  get: 1 and *value if the knob is overridden, 0 if not. */
+int hfg_debug_schedule_set(const char* knob, int value);
+int hfg_debug_schedule_clear(const char* knob);
+int hfg_debug_schedule_get(const char* knob, int* value);
+
 /* Sustained matrix-core rate of GPU `device` under a full-chip load (csrc/probe.hip):
  * 2 blocks x 4 waves per CU issue independent MFMAs back to back on random operands
  * that change every instruction, `iters` rounds of 32 MFMAs per wave (after a warm-up

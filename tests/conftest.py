@@ -12,8 +12,30 @@ if ROOT not in sys.path:
 GOLDEN_DIR = os.path.join(ROOT, "tests", "golden")
 
 
+_EVIDENCE = []
+
+
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (HIP device); run with -m gpu")
+
+
+def pytest_terminal_summary(terminalreporter):
+    """The measured numbers parity tests recorded through the `evidence` fixture (max |err|
+    against the oracle, ...), printed at the end of every run, -q included: a passing test's
+    print() output is captured and dropped, these lines are not."""
+    if _EVIDENCE:
+        terminalreporter.section("parity evidence (measured)")
+        for line in _EVIDENCE:
+            terminalreporter.write_line(line)
+
+
+@pytest.fixture
+def evidence(request):
+    """evidence(text): record one measured figure of this test for the end-of-run summary."""
+    def add(text):
+        _EVIDENCE.append(f"{request.node.nodeid}: {text}")
+        print(text)
+    return add
 
 
 @pytest.fixture(scope="session", autouse=True)
@@ -32,6 +54,17 @@ def _native_provenance(request):
 def pkg():
     import __graft_entry__ as ge
     return ge.load_package()
+
+
+@pytest.fixture
+def sched(pkg):
+    """sched(knob, value): force one schedule choice for the handles this test creates
+    (hfg_debug_schedule_set; the library reads no HFG_* environment knob); every override
+    is dropped when the test ends."""
+    def set_(knob, value):
+        pkg.schedule_override(knob, int(value))
+    yield set_
+    pkg.schedule_clear()
 
 
 @pytest.fixture(scope="session")

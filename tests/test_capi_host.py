@@ -31,7 +31,7 @@ def header_symbols():
 def test_library_exports_every_header_symbol(pkg):
     lib = pkg.load_library()
     syms = header_symbols()
-    assert len(syms) == 40
+    assert len(syms) == 43
     for s in sorted(syms):
         assert hasattr(lib, s), f"missing export {s}"
     assert set(syms) == set(pkg._lib.SIGNATURES), "ctypes signatures out of sync with headers"
@@ -524,15 +524,48 @@ def test_layer_exponent_entry_commits_or_reports(pkg):
     assert ew.value == 15 - int(np.frexp(np.abs(w).max())[1])
 
 
-def test_removed_knob_value_is_refused(pkg, monkeypatch):
-    """HFG_UPS_FRAMES=0 (the polyphase-only schedule, removed in round 4) is refused at create
-    instead of silently running the default schedule."""
+def test_removed_knob_value_is_refused(pkg):
+    """UPS_FRAMES=0 (the polyphase-only schedule, removed in round 4) is refused by the
+    schedule-override entry point instead of silently running the default schedule
+    (ADVICE r04); unknown knobs and out-of-range values are refused too."""
     lib = pkg.load_library()
     c = pkg.make_config(80, [8, 8, 2, 2], [16, 16, 4, 4], 512, [3, 7, 11], [[1, 3, 5]] * 3)
-    monkeypatch.setenv("HFG_UPS_FRAMES", "0")
-    h = ctypes.c_void_p()
-    assert lib.hfg_create(ctypes.byref(c), -1, ctypes.byref(h)) == -22
-    assert b"HFG_UPS_FRAMES" in lib.hfg_last_error()
-    monkeypatch.setenv("HFG_UPS_FRAMES", "2")
-    assert lib.hfg_create(ctypes.byref(c), -1, ctypes.byref(h)) == 0
-    lib.hfg_destroy(h)
+    try:
+        assert lib.hfg_debug_schedule_set(b"UPS_FRAMES", 0) == -22
+        assert b"UPS_FRAMES" in lib.hfg_last_error() and b"removed" in lib.hfg_last_error()
+        assert lib.hfg_debug_schedule_set(b"NO_SUCH_KNOB", 1) == -22
+        assert lib.hfg_debug_schedule_set(b"SMALL_TILE", 2) == -22
+        assert pkg.schedule_overrides() == {}
+        assert lib.hfg_debug_schedule_set(b"UPS_FRAMES", 2) == 0
+        assert pkg.schedule_overrides() == {"UPS_FRAMES": 2}
+        h = ctypes.c_void_p()
+        assert lib.hfg_create(ctypes.byref(c), -1, ctypes.byref(h)) == 0
+        lib.hfg_destroy(h)
+    finally:
+        pkg.schedule_clear()
+    assert pkg.schedule_overrides() == {}
+
+
+def _fused_flag(pkg, precision="f16x3"):
+    """info[0] of hfg_debug_packed_resblock for stage 3, ResBlock 0: 1 when the stage runs
+    whole-ResBlock launches, 0 layer by layer (the FUSED_RB schedule choice)."""
+    cfg = C.V1
+    h = host_handle(pkg, cfg, precision)
+    for k, v in C.make_state_dict(cfg, seed=3).items():
+        h.set_weight(k, torch.from_numpy(v))
+    info = (ctypes.c_int64 * 8)()
+    assert h.lib.hfg_debug_packed_resblock(h.ptr, 3, 0, None, 0, info) == 0
+    return int(info[0])
+
+
+def test_schedule_ignores_environment(pkg, monkeypatch, sched):
+    """The production handle's schedule does not depend on the caller's environment
+    (VERDICT r05 item 8): HFG_FUSED_RB=0 in the environment leaves the whole-ResBlock
+    schedule on; the override entry point (the tests' and A/B runs' path) switches it."""
+    assert _fused_flag(pkg) == 1
+    monkeypatch.setenv("HFG_FUSED_RB", "0")
+    assert _fused_flag(pkg) == 1
+    sched("FUSED_RB", 0)
+    assert _fused_flag(pkg) == 0
+    pkg.schedule_clear("FUSED_RB")
+    assert _fused_flag(pkg) == 1

@@ -113,6 +113,11 @@ def _vs_worker(rank, world, port, root, q):
         ge.load_package()
         hd = importlib.import_module(ge.PKG_NAME + ".dist")
         gen = _FakeGen()
+
+        def _no_p2p(*a, **k):
+            raise AssertionError("vocode_sharded must gather with one collective, not send/recv")
+
+        dist.send = dist.recv = _no_p2p  # this process only
         g = torch.Generator().manual_seed(5)
         lens = [int(v) for v in torch.randint(3, 20, (11,), generator=g)]
         mel = torch.randn(11, 6, max(lens), generator=g)
@@ -145,8 +150,8 @@ def _vs_worker(rank, world, port, root, q):
 
 @pytest.mark.parametrize("world", [2, 3])
 def test_gloo_vocode_sharded_gather(world):
-    """dist.vocode_sharded: length-balanced shards, per-rank forward, point-to-point
-    gather; every gathered wav equals the utterance run alone (bitwise), with the batch
+    """dist.vocode_sharded: length-balanced shards, per-rank forward, ONE dist.gather of
+    zero-padded equal-size buffers (point-to-point send/recv are patched to fail); every gathered wav equals the utterance run alone (bitwise), with the batch
     given on every rank or broadcast from one, in both mel layouts."""
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     ctx = mp.get_context("spawn")

@@ -58,7 +58,7 @@ def _window_check(cfg, sd, mel, wav, item, start, W, M):
 
 
 @pytest.mark.parametrize("precision", ["f16x3", "bf16x3", "fp32"])
-def test_c4_v2star_16x80x2048(pkg, dev, precision):
+def test_c4_v2star_16x80x2048(pkg, dev, precision, evidence):
     from oracle import config as C
     cfg = C.V2STAR
     sd = C.make_state_dict(cfg, seed=4)
@@ -70,7 +70,7 @@ def test_c4_v2star_16x80x2048(pkg, dev, precision):
     assert wav.shape == (16, 1, 2048 * 256)
     errs = [_window_check(cfg, sd, mel, wav, item, start, 40, M)
             for item, start in [(0, 0), (5, 1000), (11, 2048 - 40), (15, 517)]]
-    print(f"\nC4 [{precision}] window errors {['%.2e' % e for e in errs]}")
+    evidence(f"\nC4 [{precision}] window errors {['%.2e' % e for e in errs]}")
     assert max(errs) < ATOL
     for lo, hi in [(3, 4), (8, 13)]:
         part = _run(gen, mel[lo:hi].to(dev))
@@ -78,7 +78,7 @@ def test_c4_v2star_16x80x2048(pkg, dev, precision):
 
 
 @pytest.mark.parametrize("precision", ["f16x3", "bf16x3", "fp32"])
-def test_c3_v1_64x80x1024_one_gpu(pkg, dev, precision):
+def test_c3_v1_64x80x1024_one_gpu(pkg, dev, precision, evidence):
     from oracle import config as C
     cfg = C.V1
     sd = C.make_state_dict(cfg, seed=3)
@@ -89,7 +89,7 @@ def test_c3_v1_64x80x1024_one_gpu(pkg, dev, precision):
     assert wav.shape == (64, 1, 1024 * 256)
     errs = [_window_check(cfg, sd, mel, wav, item, start, 32, 16)
             for item, start in [(0, 0), (33, 600), (63, 1024 - 32)]]
-    print(f"\nC3 [{precision}] window errors {['%.2e' % e for e in errs]}")
+    evidence(f"\nC3 [{precision}] window errors {['%.2e' % e for e in errs]}")
     assert max(errs) < ATOL
     for r in (0, 3, 7):  # rank r's shard of the 8-GPU run
         shard = _run(gen, mel[8 * r:8 * r + 8].to(dev))
@@ -106,7 +106,7 @@ def c5():
 
 
 @pytest.mark.parametrize("precision", ["f16x3", "bf16x3", "fp32"])
-def test_c5_sambert_batch32_ragged(pkg, dev, c5, precision):
+def test_c5_sambert_batch32_ragged(pkg, dev, c5, precision, evidence):
     import importlib
     from oracle import config as C, hifigan_torch as H
     glue = importlib.import_module("tts_sambert_hifigan_amd.glue")
@@ -135,11 +135,11 @@ def test_c5_sambert_batch32_ragged(pkg, dev, c5, precision):
         err = float(np.abs(w - ref[0, 0].numpy()).max())
         worst = max(worst, err)
         assert err < ATOL, (b, err)
-    print(f"\nC5 [{precision}] 32 utterances, frames {min(lens)}-{max(lens)}: max err {worst:.2e}")
+    evidence(f"\nC5 [{precision}] 32 utterances, frames {min(lens)}-{max(lens)}: max err {worst:.2e}")
 
 
 @pytest.mark.parametrize("precision", ["f16x3", "bf16x3", "fp32"])
-def test_v2star_thin_stages_ragged_and_vs_oracle(pkg, dev, precision):
+def test_v2star_thin_stages_ragged_and_vs_oracle(pkg, dev, precision, evidence):
     """The V2* C = 16 / 8 stages run as one thin launch per MRF (csrc/mrf_thin.hip on the
     packed-fp32 VALU for C = 8 and for fp32, csrc/mrf_thin_mfma.hip for C = 16 in the split
     modes): a ragged batch equals each utterance run alone (bitwise, zero past its length),
@@ -168,4 +168,4 @@ def test_v2star_thin_stages_ragged_and_vs_oracle(pkg, dev, precision):
         err = (solo.cpu() - ref).abs().max().item()
         worst = max(worst, err)
         assert err < ATOL, b
-    print(f"\nV2* thin stages [{precision}]: max err vs oracle {worst:.2e}")
+    evidence(f"\nV2* thin stages [{precision}]: max err vs oracle {worst:.2e}")

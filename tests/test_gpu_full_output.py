@@ -1,0 +1,154 @@
+"""Every output sample against the oracle at the sizes the bench measures.
+
+* C2  V1 [8, 80, 1024] -> [8, 1, 262144] (BASELINE config 2, the headline workload): the
+      whole wav of the 2-stream schedule bench.py times (batch halves on two HIP streams,
+      `hfg_forward_ws` on a preallocated workspace, exactly bench.py's `step()`), compared
+      sample by sample with oracle/hifigan_torch.py (the reference's ATen sequence,
+      /root/reference/models/hifigan.py:224-261) in f16x3 (the headline dtype), bf16x3 and
+      exact fp32.  The module call `gen(mel)` on the same handle is bitwise the bench step,
+      and the 1-stream schedule is bitwise the 2-stream one.
+* C1  V1 [1, 80, 256] -> [1, 1, 65536] (BASELINE config 1, the latency case bench.py times
+      under extra_configs): the whole wav against the oracle, eager and as a replayed hipGraph.
+
+One oracle forward per config, shared through module fixtures (C2: ~12-25 s on the host's
+threads).  Tolerance: atol 1e-4 on the wav (BASELINE.json north_star), plus a relative-L2
+bound; the max |err| and where it occurs are printed.
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+ATOL = 1e-4
+REL_L2 = 2e-4  # secondary bar; the wav std is ~3e-3 at default init, so 1e-4 abs ~ 3e-2 rel
+
+
+@pytest.fixture(scope="module")
+def dev():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    return torch.device("cuda:0")
+
+
+def _threads():
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    return max(1, min(16, n, int(os.environ.get("OMP_NUM_THREADS", n))))
+
+
+def _oracle(cfg, sd, mel):
+    from oracle import hifigan_torch as H
+    prev = torch.get_num_threads()
+    torch.set_num_threads(_threads())
+    try:
+        with torch.no_grad():
+            return H.generator_forward(H.to_torch_state(sd), cfg, mel).numpy()
+    finally:
+        torch.set_num_threads(prev)
+
+
+@pytest.fixture(scope="module")
+def c2():
+    """Weights of seed 2, mel = randn(8, 80, 1024) of torch seed 1234 (the bench's input
+    recipe), and the oracle's whole wav."""
+    from oracle import config as C
+    cfg = C.V1
+    sd = C.make_state_dict(cfg, seed=2)
+    mel = torch.randn(8, 80, 1024, generator=torch.Generator().manual_seed(1234))
+    return cfg, sd, mel, _oracle(cfg, sd, mel)
+
+
+@pytest.fixture(scope="module")
+def c1():
+    from oracle import config as C
+    cfg = C.V1
+    sd = C.make_state_dict(cfg, seed=1)
+    mel = torch.randn(1, 80, 256, generator=torch.Generator().manual_seed(1234))
+    return cfg, sd, mel, _oracle(cfg, sd, mel)
+
+
+def _gen(pkg, cfg, sd, dev, precision):
+    gen = pkg.HiFiGANGenerator(**cfg.kwargs(), precision=precision).eval()
+    gen.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
+    return gen.to(dev)
+
+
+def _compare(tag, got, ref, evidence):
+    """max |got - ref| over every sample (asserted < ATOL) and the relative L2 error."""
+    assert got.shape == ref.shape, (got.shape, ref.shape)
+    assert np.isfinite(got).all(), tag
+    d = np.abs(got.astype(np.float64) - ref.astype(np.float64))
+    flat = int(d.argmax())
+    idx = np.unravel_index(flat, d.shape)
+    rel = float(np.sqrt((d ** 2).sum() / max((ref.astype(np.float64) ** 2).sum(), 1e-30)))
+    evidence(f"{tag}: {got.size} samples, max|hip - oracle| = {d.max():.3e} at "
+             f"{tuple(int(i) for i in idx)}, rel L2 {rel:.2e}, mean|err| {d.mean():.2e}")
+    assert d.max() < ATOL, (tag, float(d.max()), idx)
+    assert rel < REL_L2, (tag, rel)
+    return float(d.max())
+
+
+def _bench_step(gen, mel_d, dev, streams):
+    """bench.py's timed step: hfg_forward_ws on a preallocated wav and workspace, on the
+    current stream, with the handle's stream count set as bench.py sets it."""
+    h = gen.hip_handle(dev)
+    B, _, T = mel_d.shape
+    out_len = h.out_len(T)
+    h.set_streams(1)
+    ws_bytes = h.workspace_bytes(B, T)
+    h.set_streams(streams)
+    ws_bytes = max(ws_bytes, h.workspace_bytes(B, T))
+    ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
+    wav = torch.full((B, 1, out_len), float("nan"), dtype=torch.float32, device=dev)
+    st = torch.cuda.current_stream(dev)
+    h.forward_ws(mel_d.data_ptr(), B, T, wav.data_ptr(), out_len, ws.data_ptr(), ws_bytes,
+                 st.cuda_stream)
+    torch.cuda.synchronize(dev)
+    h.set_streams(2)
+    return wav
+
+
+@pytest.mark.parametrize("precision", ["f16x3", "bf16x3", "fp32"])
+def test_c2_8x80x1024_every_sample_vs_oracle(pkg, dev, c2, precision, evidence):
+    cfg, sd, mel, ref = c2
+    gen = _gen(pkg, cfg, sd, dev, precision)
+    mel_d = mel.to(dev)
+    wav2 = _bench_step(gen, mel_d, dev, streams=2)     # the schedule bench.py's value pass times
+    _compare(f"C2 [8,80,1024] {precision} 2-stream", wav2.cpu().numpy(), ref, evidence)
+    with torch.no_grad():
+        mod = gen(mel_d)                               # the drop-in module's call
+    torch.cuda.synchronize(dev)
+    assert torch.equal(mod, wav2), "gen(mel) differs from the bench step"
+    wav1 = _bench_step(gen, mel_d, dev, streams=1)     # bench.py's per-kernel (roofline) pass
+    assert torch.equal(wav1, wav2), "1-stream and 2-stream schedules differ"
+    del wav1, wav2, mod
+    torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("precision", ["f16x3", "fp32"])
+def test_c1_1x80x256_vs_oracle_eager_and_graph(pkg, dev, c1, precision, evidence):
+    cfg, sd, mel, ref = c1
+    gen = _gen(pkg, cfg, sd, dev, precision)
+    mel_d = mel.to(dev)
+    with torch.no_grad():
+        wav = gen(mel_d)
+    torch.cuda.synchronize(dev)
+    assert wav.shape == (1, 1, 65536)
+    _compare(f"C1 [1,80,256] {precision} eager", wav.cpu().numpy(), ref, evidence)
+    # bench.py extra_configs: the same forward captured once and replayed
+    s = torch.cuda.Stream(dev)
+    s.wait_stream(torch.cuda.current_stream(dev))
+    with torch.no_grad(), torch.cuda.stream(s):
+        gen(mel_d)
+    torch.cuda.current_stream(dev).wait_stream(s)
+    graph = torch.cuda.CUDAGraph()
+    with torch.no_grad(), torch.cuda.graph(graph):
+        wav_g = gen(mel_d)
+    wav_g.fill_(float("nan"))
+    graph.replay()
+    torch.cuda.synchronize(dev)
+    assert torch.equal(wav_g, wav), "hipGraph replay differs from the eager forward"

@@ -1,13 +1,11 @@
 """Small-batch launch paths on the GPU (VERDICT r01 "small-batch latency").
 
 A split-precision layer launch whose tile-3 grid would leave most CUs idle runs on the 64x64
-small-grid tile (kernels.h, tile 4; HFG_SMALL_TILE=-1 auto / 0 never / 1 always).  Every
+small-grid tile (kernels.h, tile 4; schedule knob SMALL_TILE: -1 auto / 0 never / 1 always).  Every
 output element sees the same MFMA sequence on either tile, so the choice must be bitwise
 invisible: forced-small, forced-big and auto forwards are compared with torch.equal,
 and against the oracle at the north-star 1e-4.
 """
-import os
-
 import pytest
 import torch
 
@@ -22,20 +20,18 @@ def dev():
     return torch.device("cuda:0")
 
 
-def _gen(pkg, cfg, sd, dev, precision, env):
-    old = {k: os.environ.get(k) for k in env}
-    os.environ.update(env)
+def _gen(pkg, cfg, sd, dev, precision, knobs):
+    """A module whose handle is created under the schedule overrides `knobs`
+    (hfg_debug_schedule_set; read when the handle is created, dropped right after)."""
     try:
+        for k, v in knobs.items():
+            pkg.schedule_override(k, int(v))
         gen = pkg.HiFiGANGenerator(**cfg.kwargs(), precision=precision).eval()
         gen.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
         gen = gen.to(dev)
-        gen.hip_handle(dev)  # the handle reads the environment when it is created
+        gen.hip_handle(dev)
     finally:
-        for k, v in old.items():
-            if v is None:
-                os.environ.pop(k, None)
-            else:
-                os.environ[k] = v
+        pkg.schedule_clear()
     return gen
 
 
@@ -48,7 +44,7 @@ def test_small_tile_is_bitwise_invisible(pkg, dev, preset, B, T, precision):
     mel = torch.randn(B, 80, T, generator=torch.Generator().manual_seed(B * T))
     outs = {}
     for mode in ("0", "1", "-1"):
-        gen = _gen(pkg, cfg, sd, dev, precision, {"HFG_SMALL_TILE": mode})
+        gen = _gen(pkg, cfg, sd, dev, precision, {"SMALL_TILE": mode})
         with torch.no_grad():
             outs[mode] = gen(mel.to(dev))
         torch.cuda.synchronize()
@@ -65,7 +61,7 @@ def test_small_tile_ragged_and_streaming(pkg, dev):
     from oracle import config as C
     cfg = C.V1
     sd = C.make_state_dict(cfg, seed=32)
-    gen = _gen(pkg, cfg, sd, dev, "f16x3", {"HFG_SMALL_TILE": "-1"})
+    gen = _gen(pkg, cfg, sd, dev, "f16x3", {"SMALL_TILE": "-1"})
     lens = [40, 7, 33]
     mel = torch.randn(3, 80, 40, generator=torch.Generator().manual_seed(5))
     with torch.no_grad():
@@ -78,7 +74,7 @@ def test_small_tile_ragged_and_streaming(pkg, dev):
 @pytest.mark.parametrize("precision", ["f16x3", "bf16x3", "fp32"])
 @pytest.mark.parametrize("preset,B,T", [("v1", 1, 96), ("v1", 4, 50), ("v2star", 2, 64)])
 def test_concurrent_resblocks_are_bitwise_invisible(pkg, dev, precision, preset, B, T):
-    """HFG_RB_CONC: the ResBlocks of an MRF on concurrent streams, each into its own
+    """RB_CONC: the ResBlocks of an MRF on concurrent streams, each into its own
     output, and one combine launch ((o_0 + o_1) + o_2) / 3 — the sequential epilogue's
     running sum in the same order, so the wav is bitwise unchanged."""
     from oracle import config as C
@@ -87,7 +83,7 @@ def test_concurrent_resblocks_are_bitwise_invisible(pkg, dev, precision, preset,
     mel = torch.randn(B, 80, T, generator=torch.Generator().manual_seed(T))
     outs = {}
     for mode in ("0", "1", "-1"):
-        gen = _gen(pkg, cfg, sd, dev, precision, {"HFG_RB_CONC": mode})
+        gen = _gen(pkg, cfg, sd, dev, precision, {"RB_CONC": mode})
         with torch.no_grad():
             outs[mode] = gen(mel.to(dev), lengths=[T - 3 * b for b in range(B)])
         torch.cuda.synchronize()
@@ -101,7 +97,7 @@ def test_concurrent_resblocks_hipgraph(pkg, dev):
     from oracle import config as C
     cfg = C.V1
     sd = C.make_state_dict(cfg, seed=34)
-    gen = _gen(pkg, cfg, sd, dev, "f16x3", {"HFG_RB_CONC": "1"})
+    gen = _gen(pkg, cfg, sd, dev, "f16x3", {"RB_CONC": "1"})
     gen.verify_weights = False
     mel = torch.randn(1, 80, 64, generator=torch.Generator().manual_seed(2)).to(dev)
     with torch.no_grad():
@@ -132,7 +128,7 @@ def test_ragged_batch_with_concurrent_resblocks_equals_solo(pkg, dev, preset, pr
     sd = C.make_state_dict(cfg, seed=38)
     mel = torch.randn(3, 80, 77, generator=torch.Generator().manual_seed(14))
     lens = [77, 60, 33]
-    gen = _gen(pkg, cfg, sd, dev, precision, {"HFG_RB_CONC": "1"})
+    gen = _gen(pkg, cfg, sd, dev, precision, {"RB_CONC": "1"})
     with torch.no_grad():
         out = gen(mel.to(dev), lengths=lens)
         for b, n in enumerate(lens):
@@ -146,7 +142,7 @@ def test_ragged_batch_with_concurrent_resblocks_equals_solo(pkg, dev, preset, pr
 @pytest.mark.parametrize("precision", ["bf16x3", "f16x3", "bf16w"])
 @pytest.mark.parametrize("preset", ["v1", "nonexact"])
 def test_split_resblock_is_bitwise_invisible(pkg, dev, preset, precision):
-    """HFG_RB_SPLIT=1 (default): a whole-ResBlock launch whose halo recompute the split cuts
+    """RB_SPLIT=1 (default): a whole-ResBlock launch whose halo recompute the split cuts
     by >= 10 % (k = 11 at C = 32 / 64 in V1) runs as two launches — dilation pairs {1, 3}
     writing x to scratch, then {5} with the MRF epilogue — each window paying only its own
     halo.  The fp32 round trip of x is exact, so the bf16x3 wav is bitwise unchanged (ragged
@@ -160,8 +156,8 @@ def test_split_resblock_is_bitwise_invisible(pkg, dev, preset, precision):
     mel = torch.randn(3, 80, 150, generator=torch.Generator().manual_seed(16))
     outs = {}
     for mode in ("0", "1"):
-        gen = _gen(pkg, cfg, sd, dev, precision, {"HFG_RB_SPLIT": mode, "HFG_RB_CONC": "0"})
-        conc = _gen(pkg, cfg, sd, dev, precision, {"HFG_RB_SPLIT": mode, "HFG_RB_CONC": "1"})
+        gen = _gen(pkg, cfg, sd, dev, precision, {"RB_SPLIT": mode, "RB_CONC": "0"})
+        conc = _gen(pkg, cfg, sd, dev, precision, {"RB_SPLIT": mode, "RB_CONC": "1"})
         with torch.no_grad():
             outs[mode] = gen(mel.to(dev), lengths=[150, 97, 31])
             outs[mode + "c"] = conc(mel[:1].to(dev))  # concurrent ResBlocks, per-part scratch
@@ -181,7 +177,7 @@ def test_split_resblock_is_bitwise_invisible(pkg, dev, preset, precision):
                                              ("v1", 1, 3000, None),
                                              ("nonexact", 3, 300, [300, 211, 97])])
 def test_persistent_resblock_grid_bitwise(pkg, dev, preset, B, T, lens, precision):
-    """HFG_RB_PERSIST (2, the default: a grid of n_CU blocks; 1: n_CU / stream halves): the C = 64
+    """RB_PERSIST (2, the default: a grid of n_CU blocks; 1: n_CU / stream halves): the C = 64
     ResBlock launches with the 512-column window (one block per CU) run as a persistent grid that walks the windows and copies
     each window's x to LDS beside the previous window's MRF round trip.  Every window's
     arithmetic is the one-window-per-block kernel's, so the wav is bitwise unchanged: ragged
@@ -193,7 +189,7 @@ def test_persistent_resblock_grid_bitwise(pkg, dev, preset, B, T, lens, precisio
     mel = torch.randn(B, 80, T, generator=torch.Generator().manual_seed(T + B))
     outs, names = {}, {}
     for mode in ("0", "1", "2"):  # 2: a grid of every CU per half-batch stream
-        gen = _gen(pkg, cfg, sd, dev, precision, {"HFG_RB_PERSIST": mode, "HFG_RB_CONC": "0"})
+        gen = _gen(pkg, cfg, sd, dev, precision, {"RB_PERSIST": mode, "RB_CONC": "0"})
         h = gen.hip_handle(dev)
         for n in (1, 2):
             h.set_streams(n)
@@ -220,3 +216,32 @@ def test_persistent_resblock_grid_bitwise(pkg, dev, preset, B, T, lens, precisio
             got = outs["1", 1][b:b + 1, :, a * hop:e * hop].cpu()
             assert (got - ref[:, :, off:off + (e - a) * hop]).abs().max().item() < ATOL
 
+
+
+@pytest.mark.parametrize("precision", ["f16x3", "bf16x3"])
+@pytest.mark.parametrize("rb_split", ["1", "0"])
+def test_persistent_grid_with_concurrent_resblocks_bitwise(pkg, dev, precision, rb_split):
+    """The production default (persistent C = 64 grids, RB_PERSIST=2) combined with the
+    concurrent-ResBlock schedule (RB_CONC=1: each ResBlock on its own stream with per-part
+    scratch) and with / without split k = 11 ResBlocks (RB_SPLIT; part 0 writes scratch in
+    plain-store mode): bitwise the non-persistent kernel on a one-item batch."""
+    from oracle import config as C
+    cfg = C.V1
+    sd = C.make_state_dict(cfg, seed=58)
+    mel = torch.randn(1, 80, 700, generator=torch.Generator().manual_seed(701))
+    outs, names = {}, {}
+    for mode in ("0", "2"):
+        gen = _gen(pkg, cfg, sd, dev, precision,
+                   {"RB_PERSIST": mode, "RB_CONC": "1", "RB_SPLIT": rb_split})
+        h = gen.hip_handle(dev)
+        h.profile_reset()
+        h.set_profiling(True)
+        with torch.no_grad():
+            outs[mode] = gen(mel.to(dev))
+        torch.cuda.synchronize()
+        h.set_profiling(False)
+        names[mode] = h.profile_summary()
+    assert any("persist" in k for k in names["2"]), names["2"]
+    assert not any("persist" in k for k in names["0"])
+    assert any("mrf_combine" in k for k in names["2"]), names["2"]  # the concurrent schedule ran
+    assert torch.equal(outs["0"], outs["2"]), (outs["0"] - outs["2"]).abs().max()

@@ -10,7 +10,7 @@ float64, so it is compared two ways:
 * vs ``log_mel`` (float32 torch.stft, what torchaudio computes): <= 1e-4 where the oracle
   mel >= 1e-6 x its max (measured <= 7e-5) and <= 2e-2 elsewhere — there the float32 FFT's
   own absolute error (~1e-7 of the frame energy per bin) dominates, not the device's.
-The DFT-GEMM fallback (HFG_MEL_DFT=1, n_fft not a power of two) keeps the float32 bounds
+The DFT-GEMM fallback (schedule knob MEL_DFT=1, n_fft not a power of two) keeps the float32 bounds
 of round 2.  The resampler (torchaudio Resample restated in oracle/resample_np.py, float64)
 is checked at 2e-6 x max|x|."""
 import numpy as np
@@ -107,11 +107,11 @@ def test_mel_other_fft_sizes(pkg, dev, n_fft, hop):
     assert e <= 1e-5
 
 
-def test_mel_dft_fallback(pkg, dev, monkeypatch):
-    """The DFT-GEMM path (HFG_MEL_DFT=1; the path for n_fft that are not a power of two)
+def test_mel_dft_fallback(pkg, dev, sched):
+    """The DFT-GEMM path (schedule knob MEL_DFT=1; the path for n_fft that are not a power of two)
     still meets the float32 bounds."""
     import importlib
-    monkeypatch.setenv("HFG_MEL_DFT", "1")
+    sched("MEL_DFT", "1")
     melmod = importlib.import_module("tts_sambert_hifigan_amd.mel")
     from oracle import mel_torch as M
     wav = _signals(5000)

@@ -45,7 +45,7 @@ GOLDEN = ["g1_v1_b1_t32", "g2_v1_b2_t17", "g3_v2star_b2_t32", "g4_nonexact_b1_t2
 
 
 @pytest.mark.parametrize("name", GOLDEN)
-def test_golden_fixture(pkg, golden_index, name):
+def test_golden_fixture(pkg, golden_index, name, evidence):
     dev = _dev()
     case = golden_index["cases"][name]
     cfg, sd = golden_case_state(case)
@@ -55,7 +55,7 @@ def test_golden_fixture(pkg, golden_index, name):
     assert wav.shape == g["wav"].shape
     err = np.abs(wav - g["wav"]).max()
     scale = np.abs(g["wav"]).max()
-    print(f"{name}: max|hip-ref| = {err:.3e} (max|ref| {scale:.3e})")
+    evidence(f"{name}: max|hip-ref| = {err:.3e} (max|ref| {scale:.3e})")
     assert err < ATOL
     # relative check too: a near-constant output could hide a bug
     rel = np.linalg.norm(wav - g["wav"]) / np.linalg.norm(g["wav"])
@@ -63,7 +63,7 @@ def test_golden_fixture(pkg, golden_index, name):
 
 
 @pytest.mark.parametrize("preset,B,T", [("v1", 2, 64), ("v2star", 3, 96), ("nonexact", 2, 33)])
-def test_random_vs_oracle(pkg, preset, B, T):
+def test_random_vs_oracle(pkg, preset, B, T, evidence):
     from oracle import config as C, prng
     dev = _dev()
     cfg = C.PRESETS[preset]
@@ -74,13 +74,13 @@ def test_random_vs_oracle(pkg, preset, B, T):
     ref = _oracle(cfg, sd, mel)
     assert wav.shape == ref.shape
     err = np.abs(wav - ref).max()
-    print(f"{preset} B={B} T={T}: max err {err:.3e}")
+    evidence(f"{preset} B={B} T={T}: max err {err:.3e}")
     assert err < ATOL
 
 
 @pytest.mark.parametrize("precision", ["f16x3", "bf16x3"])
 @pytest.mark.parametrize("name", GOLDEN)
-def test_golden_fixture_split(pkg, golden_index, name, precision):
+def test_golden_fixture_split(pkg, golden_index, name, precision, evidence):
     """Split-precision modes (scaled f16 / bf16 hi-lo operands, fp32 accumulate) meet the
     same 1e-4 bar against the reference outputs."""
     dev = _dev()
@@ -90,7 +90,7 @@ def test_golden_fixture_split(pkg, golden_index, name, precision):
     gen = _gen(pkg, cfg, sd, dev, precision=precision)
     wav = _run(gen, g["mel"], dev)
     err = np.abs(wav - g["wav"]).max()
-    print(f"{name} [{precision}]: max|hip-ref| = {err:.3e}")
+    evidence(f"{name} [{precision}]: max|hip-ref| = {err:.3e}")
     assert err < ATOL
     rel = np.linalg.norm(wav - g["wav"]) / np.linalg.norm(g["wav"])
     assert rel < 1e-3, rel
@@ -99,11 +99,11 @@ def test_golden_fixture_split(pkg, golden_index, name, precision):
 @pytest.mark.parametrize("precision,fused", [("f16x3", "1"), ("f16x3", "0"), ("bf16x3", "1"),
                                              ("bf16x3", "0")])
 @pytest.mark.parametrize("preset,B,T", [("v1", 2, 300), ("v2star", 2, 200)])
-def test_split_vs_oracle_longer(pkg, preset, B, T, precision, fused, monkeypatch):
+def test_split_vs_oracle_longer(pkg, preset, B, T, precision, fused, sched):
     """Random weights/mel vs the oracle with the whole-ResBlock kernel for C in {32, 64, 128}
-    on (HFG_FUSED_RB=1, default) or off (layer per launch), in both split formats."""
+    on (schedule knob FUSED_RB=1, default) or off (layer per launch), in both split formats."""
     from oracle import config as C, prng
-    monkeypatch.setenv("HFG_FUSED_RB", fused)
+    sched("FUSED_RB", fused)
     dev = _dev()
     cfg = C.PRESETS[preset]
     sd = C.make_state_dict(cfg, seed=7)
@@ -116,7 +116,7 @@ def test_split_vs_oracle_longer(pkg, preset, B, T, precision, fused, monkeypatch
 
 
 @pytest.mark.parametrize("precision", ["f16x3", "bf16x3"])
-def test_fused_resblock_matches_layer_path(pkg, precision, monkeypatch):
+def test_fused_resblock_matches_layer_path(pkg, precision, sched):
     """Whole-ResBlock kernel vs the layer-per-launch schedule on a ragged batch long enough
     for many windows per utterance (window seams, lengths that end inside a window, an
     utterance shorter than one window)."""
@@ -129,7 +129,7 @@ def test_fused_resblock_matches_layer_path(pkg, precision, monkeypatch):
     lens = torch.tensor([160, 97, 3, 131], dtype=torch.int32, device=dev)
     outs = []
     for fused in ("0", "1"):
-        monkeypatch.setenv("HFG_FUSED_RB", fused)
+        sched("FUSED_RB", fused)
         gen = _gen(pkg, cfg, sd, dev, precision=precision)
         with torch.no_grad():
             outs.append(gen(mel, lengths=lens).cpu().numpy())
@@ -203,7 +203,7 @@ def test_ragged_forward_ignores_workspace_contents(pkg, precision):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("precision,fused", [("f16x3", "1"), ("f16x3", "0"), ("bf16x3", "0")])
-def test_split_layer_kernels_run_to_run_bitwise(pkg, precision, fused, monkeypatch):
+def test_split_layer_kernels_run_to_run_bitwise(pkg, precision, fused, sched):
     """Repeated forwards are bitwise identical on every split layer-kernel tile (with the
     whole-ResBlock kernel off the 64x256 / 32x256 tiles run every C <= 64 conv).  Guards
     the per-wave vmcnt count of the staged input window (a wait that let a chunk read a
@@ -212,7 +212,7 @@ def test_split_layer_kernels_run_to_run_bitwise(pkg, precision, fused, monkeypat
     margin rows from the block maxima: forwards of other configurations (x4 weights, loud
     mels) run between the repeats."""
     from oracle import config as C, prng
-    monkeypatch.setenv("HFG_FUSED_RB", fused)
+    sched("FUSED_RB", fused)
     dev = _dev()
     cfg = C.V1
     sd = C.make_state_dict(cfg, seed=17)
@@ -249,11 +249,11 @@ def test_split_layer_kernels_run_to_run_bitwise(pkg, precision, fused, monkeypat
                                              ("v2star", 2, 64, [64, 17]),
                                              ("nonexact", 2, 64, [64, 29]),
                                              ("rates248", 3, 36, [36, 21, 5])])
-def test_ups_frames_kernel_bitwise(pkg, preset, B, T, lens, precision, monkeypatch):
+def test_ups_frames_kernel_bitwise(pkg, preset, B, T, lens, precision, sched):
     """The output-frame upsampler kernel (csrc/ups_bf16x3.hip: k = 2u stages, both sample
     classes of a frame per wave) gives the polyphase conv1d_bf16x3 upsampler's result bit
     for bit: the same MFMA sequence per output element, the same split of lrelu(x), the
-    same zero padding (and, f16x3, the same per-item input scale).  HFG_UPS_FRAMES=2 forces
+    same zero padding (and, f16x3, the same per-item input scale).  UPS_FRAMES=2 forces
     it onto every eligible stage (rates 8 and 2 in V1 / V2*, 4 and 2 in the non-exact preset;
     rate 5 stays polyphase); the default (1) keeps the polyphase small-grid tile on these
     small grids; ragged and full batches.  "rates248" puts the rate-2 stage first, so a
@@ -269,7 +269,7 @@ def test_ups_frames_kernel_bitwise(pkg, preset, B, T, lens, precision, monkeypat
     ln = torch.tensor(lens, dtype=torch.int32, device=dev)
     outs, names = {}, {}
     for mode in ("1", "2"):
-        monkeypatch.setenv("HFG_UPS_FRAMES", mode)  # read when the handle is created
+        sched("UPS_FRAMES", mode)  # read when the handle is created
         gen = _gen(pkg, cfg, sd, dev, precision=precision)
         h = gen.hip_handle(dev)
         h.profile_reset()
@@ -291,11 +291,11 @@ def test_ups_frames_kernel_bitwise(pkg, preset, B, T, lens, precision, monkeypat
 @pytest.mark.parametrize("rb_split", ["1", "0"])
 @pytest.mark.parametrize("B,T,lens", [(3, 48, [48, 29, 2]),
                                       (4, 1100, [1100, 1033, 517, 1100])])
-def test_conv_post_fused_bitwise(pkg, precision, rb_split, B, T, lens, monkeypatch):
+def test_conv_post_fused_bitwise(pkg, precision, rb_split, B, T, lens, sched):
     """conv_post + tanh fused into the last C = 32 ResBlock launch (resblock_bf16x3.hip
     conv_post_tail, the default wherever that stage runs one launch per ResBlock) gives the
     separate conv_post4_tanh kernel's wav bit for bit: the same final x on conv_post's
-    receptive field, the same (channel, tap) fma order.  HFG_RB_CONC=0 keeps the small batch
+    receptive field, the same (channel, tap) fma order.  RB_CONC=0 keeps the small batch
     on that schedule; ragged batch with whole windows past an item's end (zeroed by the
     host's memset), both split and one-launch k = 11 ResBlocks; also against the oracle.
     [4, 80, 1100] (4400 batch frames >= 4096): the forward runs as two batch halves on two
@@ -307,11 +307,11 @@ def test_conv_post_fused_bitwise(pkg, precision, rb_split, B, T, lens, monkeypat
     mel_np = prng.mel_input(53, (B, cfg.n_mels, T))
     mel = torch.as_tensor(mel_np).to(dev)
     ln = torch.tensor(lens, dtype=torch.int32, device=dev)
-    monkeypatch.setenv("HFG_RB_CONC", "0")
-    monkeypatch.setenv("HFG_RB_SPLIT", rb_split)
+    sched("RB_CONC", "0")
+    sched("RB_SPLIT", rb_split)
     outs, names = {}, {}
     for mode in ("0", "1"):
-        monkeypatch.setenv("HFG_FUSE_POST", mode)  # read when the handle is created
+        sched("FUSE_POST", mode)  # read when the handle is created
         gen = _gen(pkg, cfg, sd, dev, precision=precision)
         h = gen.hip_handle(dev)
         h.profile_reset()

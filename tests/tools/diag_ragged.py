@@ -29,10 +29,10 @@ def main():
     lens = [77, 60, 33]
     refs = [H.generator_forward(H.to_torch_state(sd), cfg, mel[b:b + 1, :, :n]).numpy()[0]
             for b, n in enumerate(lens)]
-    cases = [("f16x3", {}), ("bf16x3", {}), ("fp32", {}), ("f16x3", {"HFG_RB_CONC": "0"}),
-             ("f16x3", {"HFG_FUSED_RB": "0"}), ("f16x3", {"HFG_SMALL_TILE": "0"}),
-             ("f16x3", {"HFG_SMALL_TILE": "1"}), ("f16x3", {"HFG_UPS_FRAMES": "2"}),
-             ("fp32", {"HFG_RB_CONC": "0"})]
+    cases = [("f16x3", {}), ("bf16x3", {}), ("fp32", {}), ("f16x3", {"RB_CONC": "0"}),
+             ("f16x3", {"FUSED_RB": "0"}), ("f16x3", {"SMALL_TILE": "0"}),
+             ("f16x3", {"SMALL_TILE": "1"}), ("f16x3", {"UPS_FRAMES": "2"}),
+             ("fp32", {"RB_CONC": "0"})]
     for prec, env in cases:
         gen = _gen(pkg, cfg, sd, dev, prec, env)
         with torch.no_grad():

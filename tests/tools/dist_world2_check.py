@@ -14,7 +14,7 @@ Rank 0 prints one JSON line.  Used by tests/test_gpu_dist.py.
 HFG_DIST_BACKEND=nccl runs the same checks over RCCL (one rank per GPU: world size 1 on the
 one-GPU box): ``dist.init_process_group("nccl", device_id=...)``, the weight broadcast and the
 batch broadcast of ``vocode_sharded(..., src=0)`` on device buffers — the production path of
-``bench.py --gpus N`` and of an 8-GPU node, short of point-to-point sends between two GPUs.
+``bench.py --gpus N`` and of an 8-GPU node, short of an RCCL gather between two GPUs.
 """
 import json
 import os

@@ -11,6 +11,8 @@ pointers are valid handles for the library.
 """
 from __future__ import annotations
 
+from typing import Optional
+
 import ctypes
 import os
 from ctypes import (POINTER, c_char_p, c_double, c_int, c_int32, c_int64, c_size_t, c_void_p,
@@ -174,6 +176,9 @@ SIGNATURES = {
     "hfg_forward_taps": (c_int, [c_void_p, c_void_p, c_int64, c_int64, c_void_p, c_int64,
                                  c_void_p, c_size_t, POINTER(c_void_p), c_int, c_void_p]),
     "hfg_probe_mfma_rate": (c_int, [c_int, c_int, c_int, POINTER(c_double), POINTER(c_double)]),
+    "hfg_debug_schedule_set": (c_int, [c_char_p, c_int]),
+    "hfg_debug_schedule_clear": (c_int, [c_char_p]),
+    "hfg_debug_schedule_get": (c_int, [c_char_p, POINTER(c_int)]),
     "hfg_mel_last_error": (c_char_p, []),
     "hfg_mel_create": (c_int, [POINTER(HfgMelConfig), c_int, POINTER(c_void_p)]),
     "hfg_mel_destroy": (None, [c_void_p]),
@@ -245,6 +250,30 @@ def check(rc: int):
         msg = load_library().hfg_last_error().decode(errors="replace")
         raise HfgError(rc, msg)
     return rc
+
+
+def schedule_override(knob: str, value: int):
+    """Force one schedule choice for every handle created afterwards in this process
+    (hfg_debug_schedule_set, include/hifigan_hip_inspect.h): A/B runs and the parity suites'
+    forced paths.  The library never reads its schedule from the environment."""
+    check(load_library().hfg_debug_schedule_set(knob.encode(), int(value)))
+
+
+def schedule_clear(knob: Optional[str] = None):
+    """Drop one override (or all): later handles run the default schedule."""
+    check(load_library().hfg_debug_schedule_clear(None if knob is None else knob.encode()))
+
+
+def schedule_overrides() -> dict:
+    """The overrides in force, {knob: value}."""
+    lib = load_library()
+    out = {}
+    for k in ("FUSED_RB", "FUSE_POST", "RB_SPLIT", "SMALL_TILE", "RB_CONC", "UPS_FRAMES", "SPLIT",
+              "RB_PERSIST", "DEBUG_FLAGS", "MEL_DFT"):
+        v = c_int(0)
+        if lib.hfg_debug_schedule_get(k.encode(), ctypes.byref(v)) == 1:
+            out[k] = v.value
+    return out
 
 
 def checksum32(tensors) -> "torch.Tensor":

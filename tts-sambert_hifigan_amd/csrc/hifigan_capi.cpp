@@ -63,6 +63,48 @@ int hip_fail(hipError_t e, const char* what) {
   return fail(HFG_EIO, "%s: %s", what, hipGetErrorString(e));
 }
 
+// Schedule overrides for A/B runs and the parity suites (hfg_debug_schedule_set): a
+// process-wide table read when a handle is created.  The library reads no environment
+// variable for its schedule, so a serving process runs the default schedule whatever it
+// inherits.  Each knob: its valid range and what it selects.
+struct SchedKnob {
+  const char* name;
+  int lo, hi;
+};
+constexpr SchedKnob kSchedKnobs[] = {
+    {"FUSED_RB", 0, 1},     // whole-ResBlock kernels (0: layer by layer)
+    {"FUSE_POST", 0, 1},    // conv_post + tanh inside the last C = 32 ResBlock launch
+    {"RB_SPLIT", 0, 1},     // k = 11 whole-ResBlock launches split in two
+    {"SMALL_TILE", -1, 1},  // small-grid tile: -1 auto, 0 never, 1 always
+    {"RB_CONC", -1, 1},     // concurrent ResBlocks of small forwards: -1 auto, 0 off, 1 on
+    {"UPS_FRAMES", 1, 2},   // output-frame upsampler: 1 when its grid fills the chip, 2 always
+    {"SPLIT", 1, 2},        // batch halves on 2 HIP streams (1: one stream)
+    {"RB_PERSIST", 0, 2},   // persistent C = 64 ResBlock grids: 0 off, 1 n_CU / 2, 2 n_CU
+    {"DEBUG_FLAGS", 0, 1 << 30},  // kernel ablation bits (-DHFG_ABLATE=1 builds only)
+    {"MEL_DFT", 0, 1},      // mel: the DFT-GEMM path instead of the FFT (mel_capi.cpp)
+};
+std::mutex g_sched_mu;
+std::map<std::string, int> g_sched;
+
+const SchedKnob* sched_knob(const char* name) {
+  if (!name) return nullptr;
+  for (const SchedKnob& k : kSchedKnobs)
+    if (!strcmp(k.name, name)) return &k;
+  return nullptr;
+}
+
+// the override of `knob` into *v if one is set (else *v is left alone)
+void sched_apply(const char* knob, int* v) {
+  std::lock_guard<std::mutex> lk(g_sched_mu);
+  auto it = g_sched.find(knob);
+  if (it != g_sched.end()) *v = it->second;
+}
+void sched_apply(const char* knob, bool* v) {
+  int i = *v ? 1 : 0;
+  sched_apply(knob, &i);
+  *v = i != 0;
+}
+
 // models/hifigan.py:21-23
 int get_padding(int k, int d) { return (int)((k * d - d) / 2); }
 
@@ -1680,9 +1722,9 @@ int create_impl(const hfg_config* cfg, bool mrf_only, int device, hfg_handle** o
   h->mrf_only = mrf_only;
   h->device = device;
 #if HFG_ABLATE
-  if (const char* dbg = getenv("HFG_DEBUG_FLAGS")) h->dbg_flags = atoi(dbg);
+  sched_apply("DEBUG_FLAGS", &h->dbg_flags);
 #endif
-  if (const char* rp = getenv("HFG_RB_PERSIST")) h->rb_persist = std::min(2, std::max(0, atoi(rp)));
+  sched_apply("RB_PERSIST", &h->rb_persist);
   if (device >= 0) {
     int n = 0;
     if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess &&
@@ -1704,27 +1746,26 @@ int create_impl(const hfg_config* cfg, bool mrf_only, int device, hfg_handle** o
         if (getenv(k))
           fprintf(stderr, "[hifigan_hip] %s is set but no longer read (a removed schedule knob); "
                           "the default schedule runs\n", k);
+      // the round 1-5 environment knobs: now hfg_debug_schedule_set only
+      char env[64];
+      for (const SchedKnob& k : kSchedKnobs) {
+        snprintf(env, sizeof(env), "HFG_%s", k.name);
+        if (getenv(env))
+          fprintf(stderr, "[hifigan_hip] %s is set but the library no longer reads its schedule "
+                          "from the environment (hfg_debug_schedule_set); the default schedule "
+                          "runs\n", env);
+      }
     });
   }
   // schedule choices the parity suites compare (each bitwise invisible, or for the fused
-  // ResBlocks a different rounding order): FUSED_RB, RB_SPLIT, FUSE_POST, SMALL_TILE, RB_CONC,
-  // UPS_FRAMES, SPLIT
-  if (const char* fe = getenv("HFG_FUSED_RB")) h->use_fused_rb = atoi(fe) != 0;
-  if (const char* fp = getenv("HFG_FUSE_POST")) h->fuse_post = atoi(fp) != 0;
-  if (const char* sp = getenv("HFG_RB_SPLIT")) h->rb_split = atoi(sp) != 0;
-  if (const char* st = getenv("HFG_SMALL_TILE")) h->small_tile = atoi(st);
-  if (const char* rc = getenv("HFG_RB_CONC")) h->rb_conc = atoi(rc);
-  if (const char* uf = getenv("HFG_UPS_FRAMES")) {
-    // 0 (never the output-frame upsampler) was removed in round 4
-    const int v = atoi(uf);
-    if (v != 1 && v != 2) {
-      delete h;
-      return fail(HFG_EINVAL, "HFG_UPS_FRAMES=%s: expected 1 (default) or 2 (force the "
-                              "output-frame upsampler); 0 was removed", uf);
-    }
-    h->ups_frames = v;
-  }
-  if (const char* se = getenv("HFG_SPLIT")) h->split = atoi(se);
+  // ResBlocks a different rounding order): overridden only through hfg_debug_schedule_set
+  sched_apply("FUSED_RB", &h->use_fused_rb);
+  sched_apply("FUSE_POST", &h->fuse_post);
+  sched_apply("RB_SPLIT", &h->rb_split);
+  sched_apply("SMALL_TILE", &h->small_tile);
+  sched_apply("RB_CONC", &h->rb_conc);
+  sched_apply("UPS_FRAMES", &h->ups_frames);
+  sched_apply("SPLIT", &h->split);
   h->fmt = split_fmt(cfg->dtype);
   // bf16-valued weights: their lo plane is zero, the kernels skip lo(w) * hi(x)
   if (cfg->dtype == HFG_DTYPE_BF16W) h->np = 2;
@@ -1754,6 +1795,39 @@ const char* hfg_version(void) {
 }
 
 const char* hfg_last_error(void) { return g_err.c_str(); }
+
+int hfg_debug_schedule_set(const char* knob, int value) {
+  const SchedKnob* k = sched_knob(knob);
+  if (!k) return fail(HFG_EINVAL, "unknown schedule knob '%s'", knob ? knob : "(null)");
+  if (value < k->lo || value > k->hi)
+    return fail(HFG_EINVAL, "schedule knob %s = %d out of range [%d, %d]%s", k->name, value,
+                k->lo, k->hi,
+                !strcmp(k->name, "UPS_FRAMES") && value == 0
+                    ? " (0, the polyphase-only upsampler schedule, was removed in round 4)"
+                    : "");
+  std::lock_guard<std::mutex> lk(g_sched_mu);
+  g_sched[k->name] = value;
+  return HFG_OK;
+}
+
+int hfg_debug_schedule_clear(const char* knob) {
+  if (knob && !sched_knob(knob)) return fail(HFG_EINVAL, "unknown schedule knob '%s'", knob);
+  std::lock_guard<std::mutex> lk(g_sched_mu);
+  if (knob)
+    g_sched.erase(knob);
+  else
+    g_sched.clear();
+  return HFG_OK;
+}
+
+int hfg_debug_schedule_get(const char* knob, int* value) {
+  if (!sched_knob(knob) || !value) return fail(HFG_EINVAL, "unknown schedule knob or NULL value");
+  std::lock_guard<std::mutex> lk(g_sched_mu);
+  auto it = g_sched.find(knob);
+  if (it == g_sched.end()) return 0;
+  *value = it->second;
+  return 1;
+}
 
 int hfg_create(const hfg_config* cfg, int device, hfg_handle** out) {
   return create_impl(cfg, false, device, out);

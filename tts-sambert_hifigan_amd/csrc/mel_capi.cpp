@@ -18,6 +18,7 @@
 #include <vector>
 
 #include "../../include/hifigan_hip.h"
+#include "../../include/hifigan_hip_inspect.h"
 #include "mel_kernels.h"
 
 namespace {
@@ -226,8 +227,9 @@ int hfg_mel_create(const hfg_mel_config* c, int device, hfg_mel_handle** out) {
   h->fb_host.resize((size_t)h->n_bins * c->n_mels);
   hfg_mel_filterbank(c, h->fb_host.data());
   h->fpw = N <= 1024 ? 2 : 1;
-  const char* md = getenv("HFG_MEL_DFT");  // 1: the DFT-GEMM path (A/B and fallback tests)
-  h->fft = (N & (N - 1)) == 0 && N >= 16 && !(md && atoi(md) != 0) &&
+  int md = 0;  // 1: the DFT-GEMM path (A/B and fallback tests: hfg_debug_schedule_set)
+  hfg_debug_schedule_get("MEL_DFT", &md);
+  h->fft = (N & (N - 1)) == 0 && N >= 16 && md == 0 &&
            hfg::logmel_fft_lds_bytes(N, c->hop_length, h->fpw, c->n_mels) <= 160 * 1024;
   if (!h->fft && !dft_fits) {
     delete h;

@@ -4,7 +4,7 @@ over ranks, weights broadcast once, wavs gathered to one rank.
 The reference is single-process; utterances are independent
 (no op mixes batch items), so the collectives on this path are
 ONE broadcast of the flattened weights from rank 0 at start-up and, for the
-product call :func:`vocode_sharded`, point-to-point sends of each rank's wavs to
+product call :func:`vocode_sharded`, one gather of every rank's (padded) wavs to
 the gathering rank — ``torch.distributed`` backend "nccl" is RCCL over xGMI on
 MI355X, "gloo" on CPU for the tests.  The steady-state forward itself has no
 collective.
@@ -117,8 +117,8 @@ def vocode_sharded(gen, mel: Optional[torch.Tensor], lengths: Optional[Sequence[
     The utterances are split over the ranks by :func:`balance_by_length` (equal
     frame counts, not item counts); each rank runs ITS utterances as one ragged
     forward of ``gen`` (HiFiGANGenerator on this rank's GPU, ``hfg_forward_ex``) —
-    no collective inside the forward — and the wavs are sent point-to-point to rank
-    ``dst``.  Each wav equals the Generator run on that utterance alone (the
+    no collective inside the forward — and the wavs are collected on rank ``dst`` by
+    one ``dist.gather`` of equal-size (zero-padded) buffers.  Each wav equals the Generator run on that utterance alone (the
     ragged forward's per-utterance zero padding), so the result does not depend on
     the world size.
 
@@ -160,18 +160,21 @@ def vocode_sharded(gen, mel: Optional[torch.Tensor], lengths: Optional[Sequence[
     if dst is None:
         return mine, wavs
 
-    # gather: every rank knows every rank's items and wav lengths, so rank dst posts
-    # one receive of exactly the right size per sending rank (no size exchange)
+    # gather: every rank knows every rank's items and wav lengths, so all ranks pad their
+    # concatenated wavs to the largest rank's total and ONE dist.gather collects them on dst
+    # (RCCL: one grouped call, no size exchange, no per-pair communicators)
     cdev = _coll_device(device, group)
     parts = balance_by_length(lens, world)
-
-    def glob(r):  # send / recv take global ranks
-        return r if group is None else dist.get_global_rank(group, r)
-
+    sizes = [[gen.output_length(lens[i]) for i in parts[r]] for r in range(world)]
+    pad = max(sum(s) for s in sizes)
+    flat = torch.zeros(pad, dtype=torch.float32, device=cdev)
+    if mine:
+        flat[:sum(sizes[me])].copy_(torch.cat(wavs))
+    gdst = dst if group is None else dist.get_global_rank(group, dst)
+    bufs = ([torch.empty(pad, dtype=torch.float32, device=cdev) for _ in range(world)]
+            if me == dst else None)
+    dist.gather(flat, bufs, dst=gdst, group=group)
     if me != dst:
-        if mine:
-            flat = torch.cat(wavs).to(cdev)
-            dist.send(flat, glob(dst), group=group)
         return None
     out: List[Optional[torch.Tensor]] = [None] * B
     for n, i in enumerate(mine):
@@ -179,12 +182,9 @@ def vocode_sharded(gen, mel: Optional[torch.Tensor], lengths: Optional[Sequence[
     for r in range(world):
         if r == dst or not parts[r]:
             continue
-        sizes = [gen.output_length(lens[i]) for i in parts[r]]
-        buf = torch.empty(sum(sizes), dtype=torch.float32, device=cdev)
-        dist.recv(buf, glob(r), group=group)
-        buf = buf.to(device)
+        buf = bufs[r].to(device)
         off = 0
-        for i, s in zip(parts[r], sizes):
+        for i, s in zip(parts[r], sizes[r]):
             out[i] = buf[off:off + s]
             off += s
     return out
