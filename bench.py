@@ -147,6 +147,9 @@ def parse():
                     help="do not bracket launches with HIP events (no roofline)")
     ap.add_argument("--no-pmc", action="store_true",
                     help="skip the live rocprofv3 FETCH_SIZE / WRITE_SIZE passes (traffic=null)")
+    ap.add_argument("--sched", nargs="*", default=[], metavar="KNOB=V",
+                    help="schedule overrides for A/B runs (hfg_debug_schedule_set, e.g. "
+                         "RB_PERSIST=0); recorded in the line's config")
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
     return ap.parse_args()
 
@@ -508,7 +511,8 @@ def main():
         # before this process initialises the GPU: the passes are child processes
         print("[bench] PMC traffic passes", file=sys.stderr, flush=True)
         pmc, pmc_note = pmc_traffic(["--preset", args.preset, "--batch", str(args.batch),
-                                     "--frames", str(args.frames), "--precision", args.precision])
+                                     "--frames", str(args.frames), "--precision", args.precision]
+                                    + (["--sched"] + args.sched if args.sched else []))
     assert torch.cuda.is_available(), "bench.py needs MI355X GPUs"
     dev_index = local_rank % torch.cuda.device_count()
     torch.cuda.set_device(dev_index)
@@ -525,6 +529,9 @@ def main():
 
     pkg = ge.load_package()
     pkg.load_library()
+    for kv in args.sched:  # before any handle exists (read at hfg_create)
+        k, v = kv.split("=", 1)
+        pkg.schedule_override(k, int(v))
     import importlib
     hdist = importlib.import_module(ge.PKG_NAME + ".dist")
     S = importlib.import_module(ge.PKG_NAME + ".synth")  # random-init weights of the config
@@ -728,6 +735,7 @@ def main():
             "batch_per_gpu": args.batch,
             "frames": T,
             "global_batch": global_batch,
+            **({"schedule_overrides": dict(pkg.schedule_overrides())} if args.sched else {}),
             "parallelism": (f"dp{world} (utterance-sharded, "
                             f"{'RCCL' if args.dist_backend == 'nccl' else 'gloo'} weight broadcast at init)"
                             if use_dist else "dp1"),
