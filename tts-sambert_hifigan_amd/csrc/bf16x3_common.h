@@ -151,6 +151,20 @@ __device__ __forceinline__ float div_fast(float x, float d, float rcp) {
   return __builtin_amdgcn_classf(q0, 0x264) ? q0 : q;
 }
 
+// HFG_PRIO (round 6): a wave raises its issue priority for its matrix phase (s_setprio 1) and
+// drops it for staging / epilogue work, so a co-resident wave of ANOTHER block (2 blocks per CU)
+// that is in its MFMA loop wins the SIMD's issue arbitration over this wave's VALU burst
+// (MI355X_MICROARCH.md "Two waves per SIMD", items 2 and 4)
+#ifndef HFG_PRIO
+#define HFG_PRIO 1
+#endif
+__device__ __forceinline__ void prio_mfma() {
+  if constexpr (HFG_PRIO) __builtin_amdgcn_s_setprio(1);
+}
+__device__ __forceinline__ void prio_other() {
+  if constexpr (HFG_PRIO) __builtin_amdgcn_s_setprio(0);
+}
+
 // s_waitcnt vmcnt(N) with a compile-time N
 template <int N>
 __device__ __forceinline__ void wait_vm() {

@@ -514,6 +514,7 @@ conv1d_bf16x3(const ConvParams p) {
     };
     load_a(a0, 0, 0);
     if constexpr (AD == 2) load_a(a1, 0, 1);
+    prio_mfma();
     for (int g = 0; g < NG; ++g) {
       const __bf16* Xh = Xbuf0 + (g & 1) * xbuf;
       __bf16* const Xn = Xbuf0 + ((g + 1) & 1) * xbuf;
@@ -557,6 +558,7 @@ conv1d_bf16x3(const ConvParams p) {
 #if HFG_CONV_TIMING
     tsv[5] = bar_wait;
 #endif
+    prio_other();
     cstamp(3);
   } else if constexpr (KT_ > 0 && WM * WN >= 8) {
     // ---- 64x128-per-wave tile, compile-time taps: the chunk loop unrolled over one

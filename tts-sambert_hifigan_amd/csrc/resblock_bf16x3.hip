@@ -524,6 +524,7 @@ resblock_bf16x3(const RbParams p) {
       }
     };
     const int qb = Q0 + cv * STEPS;
+    prio_mfma();
     load_b(0, 0);
     // software pipeline: B fragments one step ahead (interleaved with this step's
     // MFMAs), A fragments two steps ahead
@@ -553,6 +554,7 @@ resblock_bf16x3(const RbParams p) {
       __builtin_amdgcn_sched_group_barrier(0x008, NP * WM * WN, 0);  // rest of the MFMAs
       __builtin_amdgcn_sched_barrier(0);
     }
+    prio_other();
   };
   // f16x3: acc = acc * 2^-(e_x + e_w) + bias (exact unscale, one rounding for the bias)
   int ex = 0;

@@ -231,6 +231,7 @@ ups_bf16x3(const UpsParams p) {
             a[c][tp][pl][i] = *reinterpret_cast<const bf16x8*>(
                 as + ((((c * 2 + tp) * 2 + pl) * WAVES_M + wave_m) * WM + i) * 1024 + lane * 16);
     const char* xh = Xbuf + (g & 1) * XBUF;
+    prio_mfma();
 #pragma unroll
     for (int k = 0; k < WN; ++k) {
       // B at tap offsets -1, 0, +1 (hi, lo)
@@ -257,6 +258,7 @@ ups_bf16x3(const UpsParams p) {
                                                                   acc[c][i][k]);
           }
     }
+    prio_other();
     if (more && !(kAblate && (p.dbg & 512))) store_x((g + 1) & 1);
     wait_vm<0>();
     lds_barrier();
