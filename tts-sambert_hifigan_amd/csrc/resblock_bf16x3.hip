@@ -48,9 +48,6 @@
 #ifndef HFG_RB_TIMING
 #define HFG_RB_TIMING 0
 #endif
-#ifndef HFG_RB_PKMUL
-#define HFG_RB_PKMUL 0
-#endif
 
 namespace hfg {
 
@@ -423,9 +420,9 @@ resblock_bf16x3(const RbParams p) {
   // The 8 accumulator rows a lane holds per 16-channel group are exactly the 8 slots
   // (one 16-B row of its half-group) it reads as a B fragment.
   // f16x3: the operand is scaled by sc = 2^e (block_exp) inside the same two factors
-  // HFG_RB_PKMUL=1: the two products of a value pair as v_pk_mul_f32 (rounds 3-5).  Packed f32
+  // Two scalar v_mul_f32 per value, not one v_pk_mul_f32 per value pair (rounds 3-5): packed f32
   // VALU costs ~22 cycles more per instruction than its two scalar halves beside MFMAs
-  // (MI355X_MICROARCH.md), so the default is two scalar v_mul_f32 per value: the same products.
+  // (MI355X_MICROARCH.md; same-box -0.9 % ResBlock time, profiles/r06/ab_rewrite.txt).
   auto write_operand = [&](const floatx16 (&v)[WM][WN], float sc) {
     if (kAblate && (dbg & 64)) return;
 #pragma unroll
@@ -439,19 +436,9 @@ resblock_bf16x3(const RbParams p) {
 #pragma unroll
           for (int e = 0; e < 8; e += 2) {
             floatx2 a;
-#if HFG_RB_PKMUL
-            floatx2 vv;
-            vv[0] = v[i][k][gg * 8 + e];
-            vv[1] = v[i][k][gg * 8 + e + 1];
-            const floatx2 f1k = f1, f2k = f2;
-            const floatx2 p1 = vv * f1k, p2 = vv * f2k;  // v_pk_mul_f32
-            a[0] = fmaxf(p1[0], p2[0]);
-            a[1] = fmaxf(p1[1], p2[1]);
-#else
             const float v0 = v[i][k][gg * 8 + e], v1 = v[i][k][gg * 8 + e + 1];
             a[0] = fmaxf(v0 * f1, v0 * f2);
             a[1] = fmaxf(v1 * f1, v1 * f2);
-#endif
             bf16x2 hh, ll;
             split2<FMT>(a, hh, ll);
             h[e] = hh[0];
