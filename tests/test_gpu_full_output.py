@@ -9,6 +9,10 @@
       and the 1-stream schedule is bitwise the 2-stream one.
 * C1  V1 [1, 80, 256] -> [1, 1, 65536] (BASELINE config 1, the latency case bench.py times
       under extra_configs): the whole wav against the oracle, eager and as a replayed hipGraph.
+* C4  pinned V2* [16, 80, 2048] -> [16, 1, 524288] (BASELINE config 4): every
+      one of its 8,388,608 samples against the oracle (~12 s on 8 host threads).
+  (C3 [64, 80, 1024] = eight C2-shaped shards, each bitwise its standalone forward:
+  tests/test_gpu_configs.py; its 16.8 M-sample oracle would take minutes of host time.)
 
 One oracle forward per config, shared through module fixtures (C2: ~12-25 s on the host's
 threads).  Tolerance: atol 1e-4 on the wav (BASELINE.json north_star), plus a relative-L2
@@ -59,6 +63,15 @@ def c2():
     cfg = C.V1
     sd = C.make_state_dict(cfg, seed=2)
     mel = torch.randn(8, 80, 1024, generator=torch.Generator().manual_seed(1234))
+    return cfg, sd, mel, _oracle(cfg, sd, mel)
+
+
+@pytest.fixture(scope="module")
+def c4():
+    from oracle import config as C
+    cfg = C.V2STAR
+    sd = C.make_state_dict(cfg, seed=4)
+    mel = torch.randn(16, 80, 2048, generator=torch.Generator().manual_seed(1234))
     return cfg, sd, mel, _oracle(cfg, sd, mel)
 
 
@@ -152,3 +165,14 @@ def test_c1_1x80x256_vs_oracle_eager_and_graph(pkg, dev, c1, precision, evidence
     graph.replay()
     torch.cuda.synchronize(dev)
     assert torch.equal(wav_g, wav), "hipGraph replay differs from the eager forward"
+
+
+@pytest.mark.parametrize("precision", ["f16x3", "fp32"])
+def test_c4_v2star_16x80x2048_every_sample_vs_oracle(pkg, dev, c4, precision, evidence):
+    cfg, sd, mel, ref = c4
+    gen = _gen(pkg, cfg, sd, dev, precision)
+    wav = _bench_step(gen, mel.to(dev), dev, streams=2)
+    assert wav.shape == (16, 1, 2048 * 256)
+    _compare(f"C4 V2* [16,80,2048] {precision} 2-stream", wav.cpu().numpy(), ref, evidence)
+    del wav
+    torch.cuda.empty_cache()
