@@ -22,13 +22,14 @@ def dev():
     return torch.device("cuda:0")
 
 
-STREAM_F16X3_TOL = 1e-7  # f16x3 stream vs one-shot (measured ~1.5e-8); exact modes: bitwise
-# ... relative to the largest activation M of the network (the f16x3 scales are powers of two
-# of a launch's max, and a value below 2^-17 of that max keeps an absolute error <= 2^-39 of
-# it; one conv sums ~C.k such terms): the bound is max(1e-7, 2^-25 * M) — 1e-7 at default scale
-# (M ~ 2.7) — exercised louder by test_streaming_loud_relative_bound (2x weights: unsaturated
-# tanh; 4x weights and a 3x mel: M ~ 2e6, saturated)
-STREAM_F16X3_REL = 2.0 ** -25
+STREAM_F16X3_TOL = 1e-7  # f16x3 stream vs one-shot at default scale (measured 0-1.5e-8)
+# Away from default scale the f16x3 stream and the one-shot run are two evaluations with
+# different power-of-two operand scales (a window's max vs the utterance's), each within the
+# mode's accuracy of the exact result, and their difference grows with that accuracy (2x
+# weights: 4.8e-7, round 6).  The contract there: the stream is as accurate as the one-shot run
+# — max|stream - oracle| <= 2 x max|one-shot - oracle| + 1e-7
+# (test_streaming_loud_relative_bound); the exact modes stay bitwise at every scale.
+STREAM_F16X3_ACC = 2.0
 
 
 def randn(*shape, seed, dev):
@@ -102,18 +103,10 @@ def _stage_exponents(sd, mel):
     return ex
 
 
-def _stage_max(sd, mel, cfg):
-    """max |value| of every oracle stage tap (conv_pre, ups.i, mrfs.i, wav)."""
-    from oracle import hifigan_torch as H
-    mx = {}
-    H.generator_forward(H.to_torch_state(sd), cfg, mel.cpu()[None],
-                        tap=lambda n, t: mx.__setitem__(n, t.abs().max().item()))
-    return mx
-
-
-def _check_stream(gen, sd, mel, out, windows, label, cfg=None, evidence=print):
+def _check_stream(gen, sd, mel, out, windows, label, cfg=None, evidence=print, strict=True):
     """The streaming contract for one stream: every chunk bitwise the crop of gen(window);
-    the stream bitwise (fp32, bf16x3) / within 1e-7 (f16x3) of the one-shot run, with the
+    the stream bitwise (fp32, bf16x3) the one-shot run, and in f16x3 within 1e-7 of it at
+    default scale (strict) / as accurate as it against the oracle (any scale), with the
     evidence printed (max |diff|, differing samples, first one, the chunk's and the one-shot
     run's stage exponents); within 1e-4 of the oracle."""
     from oracle import config as C, hifigan_torch as H
@@ -138,17 +131,17 @@ def _check_stream(gen, sd, mel, out, windows, label, cfg=None, evidence=print):
         a, b, lo, hi = worst[1]
         msg += (f"; worst chunk frames [{a}, {b}) window [{lo}, {hi}): stage exponents window "
                 f"{_stage_exponents(sd, mel[:, lo:hi])} vs one-shot {_stage_exponents(sd, mel)}")
-    evidence(msg)
-    if gen.precision == "f16x3":
-        big = max(_stage_max(sd, mel, cfg).values())
-        tol = max(STREAM_F16X3_TOL, STREAM_F16X3_REL * big)
-        evidence(f"{label}: largest activation {big:.3e}: bound {tol:.3e}, max|diff| = "
-                 f"{dmax / big:.3e} of it")
-        assert dmax <= tol, msg
-    else:
-        assert n_diff == 0, msg
     o = H.generator_forward(H.to_torch_state(sd), cfg, mel.cpu()[None])[0, 0]
     err = (out.cpu() - o).abs().max().item()
+    err_one = (ref.cpu() - o).abs().max().item()
+    msg += f"; vs oracle: stream {err:.3e}, one-shot {err_one:.3e}"
+    evidence(msg)
+    if gen.precision == "f16x3":
+        if strict:
+            assert dmax <= STREAM_F16X3_TOL, msg
+        assert err <= STREAM_F16X3_ACC * err_one + STREAM_F16X3_TOL, msg
+    else:
+        assert n_diff == 0, msg
     assert err < ATOL, (label, err)
 
 
@@ -195,12 +188,12 @@ def test_streaming_equals_one_shot(pkg, gen_sd, dev, evidence):
 
 @pytest.mark.parametrize("wscale,mscale", [(2.0, 1.0), (4.0, 3.0)])
 def test_streaming_loud_relative_bound(pkg, dev, evidence, wscale, mscale):
-    """The f16x3 stream-vs-one-shot bound away from default scale: 2x weights
-    (activations ~1e2-1e3, tanh not saturated: the g6 fixture's regime) and 4x weights with a 3x
-    mel (activations ~2e6, tanh saturated), chunks of 40 frames pushed in random pieces.  Every
-    chunk is still bitwise its window's crop; the stream is within max(1e-7, 2^-25 x the largest
-    activation) of the one-shot run (printed as a fraction of that activation) and within 1e-4 of
-    the oracle; fp32 and bf16x3 stay bitwise."""
+    """The f16x3 streaming contract away from default scale: 2x weights (tanh not
+    saturated: the g6 fixture's regime; the stream differs from the one-shot run by up to ~5e-7
+    there, round 6) and 4x weights with a 3x mel (stage maxima ~2e6, tanh saturated), chunks of
+    40 frames pushed in random pieces.  Every chunk is still bitwise its window's crop; the stream
+    is as accurate as the one-shot run (max |stream - oracle| <= 2 x max |one-shot - oracle| +
+    1e-7) and within 1e-4 of the oracle; fp32 and bf16x3 stay bitwise."""
     import importlib
     glue = importlib.import_module("tts_sambert_hifigan_amd.glue")
     from oracle import config as C
@@ -212,7 +205,8 @@ def test_streaming_loud_relative_bound(pkg, dev, evidence, wscale, mscale):
         gen = gen.to(dev)
         out, windows = _stream_once(glue, gen, mel, 40, 11)
         _check_stream(gen, sd, mel, out, windows,
-                      f"weights x{wscale:g} mel x{mscale:g} [{precision}]", evidence=evidence)
+                      f"weights x{wscale:g} mel x{mscale:g} [{precision}]", evidence=evidence,
+                      strict=False)
 
 
 def test_streaming_is_deterministic_across_unrelated_forwards(pkg, gen_sd, dev):
