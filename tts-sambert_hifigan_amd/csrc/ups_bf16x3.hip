@@ -213,12 +213,14 @@ ups_bf16x3(const UpsParams p) {
   const int colw = wave_n * 32 * WN + col + 4;
   for (int g = 0; g < NG; ++g) {
     const bool more = g + 1 < NG;  // block-uniform
+    // ablation bit 17 (timing only): no weight slab after group 0's (every group re-reads it)
+    const bool slab0 = kAblate && (p.dbg & 131072);
     if (more) {
-      issue_a(g + 1, (g + 1) & 1);
+      if (!slab0) issue_a(g + 1, (g + 1) & 1);
       if (!(kAblate && (p.dbg & 1024))) load_x(g + 1);
     }
     // A fragments of both classes and taps: [class][tap][plane][wm]
-    const char* as = Abuf + (g & 1) * SLAB;
+    const char* as = Abuf + (slab0 ? 0 : (g & 1)) * SLAB;
     bf16x8 a[2][2][2][WM];
 #pragma unroll
     for (int c = 0; c < 2; ++c)
@@ -306,7 +308,7 @@ ups_bf16x3(const UpsParams p) {
             v.y = odd ? v1 : r0;
             v.z = odd ? l1 : v0;
             v.w = odd ? r1 : v1;
-            *reinterpret_cast<float4*>(yb + (int64_t)(odd ? co0 + 1 : co0) * p.L_out + 2 * me) = v;
+            if (!(kAblate && (p.dbg & 262144))) *reinterpret_cast<float4*>(yb + (int64_t)(odd ? co0 + 1 : co0) * p.L_out + 2 * me) = v;
             t2(v.x, v.y);
             t2(v.z, v.w);
           } else {
@@ -317,8 +319,8 @@ ups_bf16x3(const UpsParams p) {
             a[1] = r0;
             c[0] = l1;
             c[1] = r1;
-            *reinterpret_cast<floatx2*>(yb + (int64_t)co0 * p.L_out + 2 * m) = a;
-            *reinterpret_cast<floatx2*>(yb + (int64_t)(co0 + 1) * p.L_out + 2 * m) = c;
+            if (!(kAblate && (p.dbg & 262144))) *reinterpret_cast<floatx2*>(yb + (int64_t)co0 * p.L_out + 2 * m) = a;
+            if (!(kAblate && (p.dbg & 262144))) *reinterpret_cast<floatx2*>(yb + (int64_t)(co0 + 1) * p.L_out + 2 * m) = c;
             t2(l0, r0);
             t2(l1, r1);
           }
@@ -332,7 +334,7 @@ ups_bf16x3(const UpsParams p) {
           floatx2 v;
           v[0] = __builtin_fmaf(acc[0][i][k][r], sc, bv);
           v[1] = __builtin_fmaf(acc[1][i][k][r], sc, bv);
-          *reinterpret_cast<floatx2*>(yb + (int64_t)co * p.L_out + 2 * m) = v;
+          if (!(kAblate && (p.dbg & 262144))) *reinterpret_cast<floatx2*>(yb + (int64_t)co * p.L_out + 2 * m) = v;
           t2(v[0], v[1]);
         }
       } else if (h == 2) {
@@ -349,7 +351,7 @@ ups_bf16x3(const UpsParams p) {
             v.y = __builtin_fmaf(acc[0][i][k][r0 + 1], sc, bv);
             v.z = __builtin_fmaf(acc[1][i][k][r0], sc, bv);
             v.w = __builtin_fmaf(acc[1][i][k][r0 + 1], sc, bv);
-            *reinterpret_cast<float4*>(yb + (int64_t)co * p.L_out + 4 * m) = v;
+            if (!(kAblate && (p.dbg & 262144))) *reinterpret_cast<float4*>(yb + (int64_t)co * p.L_out + 4 * m) = v;
             t2(v.x, v.y);
             t2(v.z, v.w);
           }
@@ -367,7 +369,7 @@ ups_bf16x3(const UpsParams p) {
             v.y = __builtin_fmaf(acc[c][i][k][4 * q + 1], sc, bv);
             v.z = __builtin_fmaf(acc[c][i][k][4 * q + 2], sc, bv);
             v.w = __builtin_fmaf(acc[c][i][k][4 * q + 3], sc, bv);
-            *reinterpret_cast<float4*>(yb + (int64_t)co * p.L_out + m * p.u + c * h + sp) = v;
+            if (!(kAblate && (p.dbg & 262144))) *reinterpret_cast<float4*>(yb + (int64_t)co * p.L_out + m * p.u + c * h + sp) = v;
             t2(v.x, v.y);
             t2(v.z, v.w);
           }
