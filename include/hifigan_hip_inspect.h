@@ -53,7 +53,8 @@ int hfg_forward_taps(hfg_handle* h, const float* mel, int64_t B, int64_t T, floa
  * variable for its schedule (the HFG_* knobs of rounds 1-5 are only warned about), so a
  * production handle runs the default schedule whatever its process inherits.  Knobs:
  * FUSED_RB 0|1, FUSE_POST 0|1, RB_SPLIT 0|1, SMALL_TILE -1|0|1, RB_CONC -1|0|1,
- * UPS_FRAMES 1|2, SPLIT 1|2, RB_PERSIST 0..2, DEBUG_FLAGS (ablation builds), MEL_DFT 0|1.
+ * UPS_FRAMES 1|2, SPLIT 1|2, RB_PERSIST 0..2, DEBUG_FLAGS (ablation builds), MEL_DFT 0|1,
+ * AREG_TALL 0|1.
  * set: HFG_EINVAL for an unknown knob or a value out of range.  clear: one knob, or all
  * with knob == NULL.  get: 1 and *value if the knob is overridden, 0 if not. */
 int hfg_debug_schedule_set(const char* knob, int value);

@@ -228,7 +228,8 @@ SPLIT_TOL = {"bf16x3": 2.0 ** -15, "f16x3": 2.0 ** -21}
 def test_split_packing(pkg, preset, precision):
     """Split-precision layers: the packed hi/lo planes reconstruct every weight to ~2^-16
     (bf16x3) / ~2^-22 (f16x3, after the layer's 2^-ew) relative, in the fragment order of
-    conv_bf16x3.hip (tile 5 for the layer convs of M >= 128, tiles 1 / 2 below)."""
+    conv_bf16x3.hip (tile 6 for the 256-row layer convs, tile 5 for the other M >= 128, tiles 1 / 2
+    below)."""
     cfg = C.PRESETS[preset]
     sd = C.make_state_dict(cfg, seed=31)
     h = host_handle(pkg, cfg, precision)
@@ -236,7 +237,8 @@ def test_split_packing(pkg, preset, precision):
         h.set_weight(k, torch.from_numpy(v))
     h.commit()
     # tile -> (WAVES_M, WM, TPC)
-    WAVES = {0: (2, 2, 4), 1: (1, 2, 2), 2: (1, 1, 4), 3: (2, 2, 2), 4: (2, 1, 4), 5: (2, 2, 2)}
+    WAVES = {0: (2, 2, 4), 1: (1, 2, 2), 2: (1, 1, 4), 3: (2, 2, 2), 4: (2, 1, 4), 5: (2, 2, 2),
+             6: (4, 2, 2)}
     n_checked = 0
     for mod in ["conv_pre", "mrfs.0.resblocks.2.convs1.1", "mrfs.1.resblocks.0.convs2.1",
                 "mrfs.2.resblocks.1.convs1.0", "mrfs.3.resblocks.2.convs2.1"]:
@@ -483,7 +485,7 @@ def test_bf16w_packing(pkg, preset):
             assert info["tile"] != 0, mod
             n_split += 1
             u = packed.view(np.uint16)
-            TPC = {0: 4, 1: 2, 2: 4, 3: 2, 4: 4, 5: 2}[info["tile"]]
+            TPC = {0: 4, 1: 2, 2: 4, 3: 2, 4: 4, 5: 2, 6: 2}[info["tile"]]
             planes = u.reshape(-1, TPC, 2, u.size // (info["m_tiles"] * info["n_chunks"] * TPC * 2))
             assert not planes[:, :, 1].any(), f"{mod}: lo plane not zero"
             hi = np.sort(dec(planes[:, :, 0], "bf16w", info["ew"]).astype(np.float32).ravel())

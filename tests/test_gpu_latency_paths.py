@@ -245,3 +245,34 @@ def test_persistent_grid_with_concurrent_resblocks_bitwise(pkg, dev, precision, 
     assert not any("persist" in k for k in names["0"])
     assert any("mrf_combine" in k for k in names["2"]), names["2"]  # the concurrent schedule ran
     assert torch.equal(outs["0"], outs["2"]), (outs["0"] - outs["2"]).abs().max()
+
+
+@pytest.mark.parametrize("precision", ["f16x3", "bf16x3", "bf16w"])
+def test_tall_areg_tile_bitwise(pkg, dev, precision):
+    """The 256x128 AREG tile (6: the 256-row stage-0 layer convs of V1, round 6) against tile 5
+    (schedule knob AREG_TALL=0): every output element sees the same MFMA sequence (channel groups
+    x taps in order, lo*hi, hi*lo, hi*hi), so the wav is bitwise the same — full and ragged
+    batches, two streams included."""
+    from oracle import config as C
+    cfg = C.V1
+    sd = C.make_state_dict(cfg, seed=61)
+    # 8 items x 1100 frames: each batch-half stream's stage-0 grid (4 x 69 column tiles of 128)
+    # stays above the small-grid threshold, so the layer convs run on tiles 6 / 5
+    mel = torch.randn(8, 80, 1100, generator=torch.Generator().manual_seed(62))
+    lens = [1100, 517, 3, 1034, 1100, 1100, 800, 1099]
+    outs, names = {}, {}
+    for mode in ("0", "1"):
+        gen = _gen(pkg, cfg, sd, dev, precision, {"AREG_TALL": mode})
+        h = gen.hip_handle(dev)
+        h.profile_reset()
+        h.set_profiling(True)
+        with torch.no_grad():
+            outs[mode] = (gen(mel.to(dev)), gen(mel.to(dev), lengths=lens))
+        torch.cuda.synchronize()
+        h.set_profiling(False)
+        names[mode] = h.profile_summary()
+    tall = [k for k in names["1"] if k.startswith("conv1d_bf16x3<") and ", 4, 1, 2, 4, 2," in k]
+    assert tall, names["1"]
+    assert not any(", 4, 1, 2, 4, 2," in k for k in names["0"])
+    for a, b in zip(outs["0"], outs["1"]):
+        assert torch.equal(a, b), (a - b).abs().max()

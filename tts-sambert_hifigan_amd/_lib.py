@@ -269,7 +269,7 @@ def schedule_overrides() -> dict:
     lib = load_library()
     out = {}
     for k in ("FUSED_RB", "FUSE_POST", "RB_SPLIT", "SMALL_TILE", "RB_CONC", "UPS_FRAMES", "SPLIT",
-              "RB_PERSIST", "DEBUG_FLAGS", "MEL_DFT"):
+              "RB_PERSIST", "DEBUG_FLAGS", "MEL_DFT", "AREG_TALL"):
         v = c_int(0)
         if lib.hfg_debug_schedule_get(k.encode(), ctypes.byref(v)) == 1:
             out[k] = v.value

@@ -405,10 +405,9 @@ conv1d_bf16x3(const ConvParams p) {
 #endif
   // AREG: the m-tile's bias in LDS for the epilogue (conv_epilogue_lds2), visible after the
   // prologue barrier
-  static_assert(!AREG || (WAVES_M == kBf16x3Tiles[5].WAVES_M && WAVES_N == kBf16x3Tiles[5].WAVES_N &&
-                          WM == kBf16x3Tiles[5].WM && WN == kBf16x3Tiles[5].WN),
-                "AREG = tile 5 (the host sizes its LDS from that configuration)");
-  constexpr int BIAS_OFF = AREG ? bf16x3_areg_bias_off(KT_MAX, kBf16x3Tiles[5]) : 0;
+  // the AREG tiles (5, 6): the host sizes the LDS from the same configuration
+  constexpr Bf16x3Cfg TCFG{WAVES_M, WAVES_N, WM, WN, TPC, WD, AREG ? 1 : 0};
+  constexpr int BIAS_OFF = AREG ? bf16x3_areg_bias_off(KT_MAX, TCFG) : 0;
   float* const bias_lds = reinterpret_cast<float*>(reinterpret_cast<char*>(lds16) + BIAS_OFF);
   if constexpr (AREG)
     for (int i = tid; i < MT; i += NT) bias_lds[i] = p.bias[mt * MT + i];
@@ -860,8 +859,8 @@ struct Entry3 {
   HFG3_VARIANTS(KT, 1, UPS), HFG3_VARIANTS(KT, 2, UPS), HFG3_VARIANTS(KT, 3, UPS),     \
       HFG3_VARIANTS(KT, 4, UPS)
 
-// tile 5 (AREG): compile-time taps, layer convs only
-#define HFG3_AREG(KT) HFG3_VARIANTS(KT, 5, false)
+// tiles 5 and 6 (AREG): compile-time taps, layer convs only
+#define HFG3_AREG(KT) HFG3_VARIANTS(KT, 5, false), HFG3_VARIANTS(KT, 6, false)
 Entry3 g_entries3[] = {
     HFG3_TILES(3, false), HFG3_TILES(5, false), HFG3_TILES(7, false), HFG3_TILES(11, false),
     HFG3_TILES(0, false), HFG3_TILES(2, true),  HFG3_TILES(0, true),

@@ -82,6 +82,7 @@ constexpr SchedKnob kSchedKnobs[] = {
     {"RB_PERSIST", 0, 2},   // persistent C = 64 ResBlock grids: 0 off, 1 n_CU / 2, 2 n_CU
     {"DEBUG_FLAGS", 0, 1 << 30},  // kernel ablation bits (-DHFG_ABLATE=1 builds only)
     {"MEL_DFT", 0, 1},      // mel: the DFT-GEMM path instead of the FFT (mel_capi.cpp)
+    {"AREG_TALL", 0, 1},    // 256-row layers on the 256x128 AREG tile (6) instead of tile 5
 };
 std::mutex g_sched_mu;
 std::map<std::string, int> g_sched;
@@ -226,6 +227,9 @@ struct hfg_handle {
   int dbg_flags = 0;  // HFG_DEBUG_FLAGS (kernel ablations, -DHFG_ABLATE=1 builds only)
   // HFG_RB_PERSIST (default 2): persistent grids for the one-block-per-CU ResBlock launches
   int rb_persist = 2;
+  // AREG_TALL: layers whose rows are a multiple of 256 on the 256x128 AREG tile (6): each input
+  // window staged once per 128 output columns instead of once per m-tile (bitwise tile 5)
+  int areg_tall = 1;
   int n_cu = 256;      // compute units of the device (hipDeviceAttributeMultiprocessorCount)
   int halves = 1;      // batch halves of the running forward (2: two streams share the CUs)
   // batch split over two HIP streams (HFG_SPLIT=1 disables): the two halves' launches
@@ -399,7 +403,9 @@ int build_layers(hfg_handle* h) {
       // count has a compile-time instance, whole 16-channel groups
       if (L.tile == 3 && L.kind == L_CONV && L.C_in % 16 == 0 &&
           (L.KT == 3 || L.KT == 5 || L.KT == 7 || L.KT == 11))
-        L.tile = hfg::kAregTile;
+        L.tile = h->areg_tall && L.M % hfg::kBf16x3Tiles[hfg::kAregTallTile].MT() == 0
+                     ? hfg::kAregTallTile
+                     : hfg::kAregTile;
       const hfg::Bf16x3Cfg& t3 = hfg::kBf16x3Tiles[L.tile];
       L.prec = 1;
       L.CK = hfg::kBf16x3Ck;
@@ -1766,6 +1772,7 @@ int create_impl(const hfg_config* cfg, bool mrf_only, int device, hfg_handle** o
   sched_apply("RB_CONC", &h->rb_conc);
   sched_apply("UPS_FRAMES", &h->ups_frames);
   sched_apply("SPLIT", &h->split);
+  sched_apply("AREG_TALL", &h->areg_tall);
   h->fmt = split_fmt(cfg->dtype);
   // bf16-valued weights: their lo plane is zero, the kernels skip lo(w) * hi(x)
   if (cfg->dtype == HFG_DTYPE_BF16W) h->np = 2;

@@ -129,7 +129,7 @@ struct Bf16x3Cfg {
   constexpr int NTILE() const { return 32 * WN * WAVES_N; }
   constexpr int threads() const { return 64 * WAVES_M * WAVES_N; }
 };
-constexpr int kBf16x3Tiles_n = 6;
+constexpr int kBf16x3Tiles_n = 7;
 // 0: (removed in round 4: 128x256, 2x4 waves of 64x64, 3-deep weight ring, 1 block/CU —
 //    slower than tile 3 / 5; the slot keeps the other tiles' indices)
 // 1: 64x256, 1x4 waves of 64x64, 2 taps/chunk (2 blocks/CU)
@@ -144,10 +144,15 @@ constexpr int kBf16x3Tiles_n = 6;
 //    (L2) into registers two taps ahead instead of through an LDS slab ring: LDS holds
 //    only the input windows, and the block synchronises once per channel group instead
 //    of once per 2-tap chunk (layer convs with compile-time taps; HFG_AREG)
+// 6: tile 5's schedule on a 256x128 block, 4x1 waves of 64x128 (round 6; layers with 256
+//    output rows: one m-tile, so each input window is staged once per 128 output columns
+//    instead of twice per 256 — half the staging loads and conversions per output; every
+//    wave reads its own A rows: twice tile 5's A traffic from L2)
 constexpr Bf16x3Cfg kBf16x3Tiles[kBf16x3Tiles_n] = {
     {2, 4, 2, 2, 4, 3, 0}, {1, 4, 2, 2, 2, 2, 0}, {1, 4, 1, 2, 4, 2, 0}, {2, 2, 2, 4, 2, 2, 0},
-    {2, 1, 1, 2, 4, 2, 0}, {2, 2, 2, 4, 2, 2, 1}};
+    {2, 1, 1, 2, 4, 2, 0}, {2, 2, 2, 4, 2, 2, 1}, {4, 1, 2, 4, 2, 2, 1}};
 constexpr int kAregTile = 5;
+constexpr int kAregTallTile = 6;
 constexpr int kBf16x3SmallTile = 4;
 // a layer launch runs on the small tile when its tile-3 grid has fewer blocks than this
 // (tile 3 fits 2 blocks per CU: 512 slots on 256 CUs)
