@@ -28,7 +28,7 @@ STREAM_F16X3_TOL = 1e-7  # f16x3 stream vs one-shot at default scale (measured 0
 # mode's accuracy of the exact result, and their difference grows with that accuracy (2x
 # weights: 4.8e-7, round 6).  The contract there: the stream is as accurate as the one-shot run
 # — max|stream - oracle| <= 2 x max|one-shot - oracle| + 1e-7
-# (test_streaming_loud_relative_bound); the exact modes stay bitwise at every scale.
+# (test_streaming_accuracy_away_from_default_scale); the exact modes stay bitwise at every scale.
 STREAM_F16X3_ACC = 2.0
 
 
@@ -187,7 +187,7 @@ def test_streaming_equals_one_shot(pkg, gen_sd, dev, evidence):
 
 
 @pytest.mark.parametrize("wscale,mscale", [(2.0, 1.0), (4.0, 3.0)])
-def test_streaming_loud_relative_bound(pkg, dev, evidence, wscale, mscale):
+def test_streaming_accuracy_away_from_default_scale(pkg, dev, evidence, wscale, mscale):
     """The f16x3 streaming contract away from default scale: 2x weights (tanh not
     saturated: the g6 fixture's regime; the stream differs from the one-shot run by up to ~5e-7
     there, round 6) and 4x weights with a 3x mel (stage maxima ~2e6, tanh saturated), chunks of
