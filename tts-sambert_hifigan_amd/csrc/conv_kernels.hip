@@ -487,31 +487,47 @@ hipError_t launch_stage_lengths(const int32_t* lens, int B, const StageLenParams
 // y = (((o_0 + o_1) + o_2) + ...) / n, the same additions in the same order as the
 // sequential schedule's epilogue running sum, so the result is bitwise the same.
 // float4 over [B][C][L] rows (L % 4 == 0) with a scalar tail; columns past len[b] skipped.
-__global__ void __launch_bounds__(256) mrf_combine_kernel(MrfCombineArgs a) {
-  const int b = blockIdx.y;
+// An item holds < 2^30 elements (the C ABI's limit), so offsets within it are 32-bit.  The
+// grid is capped near two blocks per CU and each block folds its max into one atomic: the
+// item's kAmaxSpread scale words sit in one L2 channel, and one atomic per wave of a grid
+// that finishes all at once serialised there (round 6: 48 us for 8192 waves at C1).
+#ifndef HFG_COMBINE_BLOCKS
+#define HFG_COMBINE_BLOCKS 512
+#endif
+template <int NMAX>
+__device__ __forceinline__ void mrf_combine_body(const MrfCombineArgs& a, int b, float& vmax) {
   const int len_b = a.len ? min(a.len[b], a.L) : a.L;
   const int64_t base = (int64_t)b * a.C * a.L;
-  const int64_t n = (int64_t)a.C * a.L;
-  float vmax = 0.f;  // max |stored value| (f16x3 consumers: a.amax_out)
-  for (int64_t i = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4; i < n;
-       i += (int64_t)gridDim.x * 256 * 4) {
-    const int t = (int)(i % a.L);
+  const int n = a.C * a.L;
+  const float* o[NMAX];
+#pragma unroll
+  for (int j = 0; j < NMAX; ++j) o[j] = a.o[j < a.n ? j : 0] + base;
+  float* y = a.y + base;
+  const int stride = gridDim.x * 256 * 4;
+  for (int i = (blockIdx.x * 256 + threadIdx.x) * 4; i < n; i += stride) {
+    const int t = i % a.L;
     if ((a.L & 3) == 0) {
       // 4 samples of one channel row (L % 4 == 0): one test for the group
       if (t >= len_b) continue;
-      float4 acc = *reinterpret_cast<const float4*>(a.o[0] + base + i);
-      for (int j = 1; j < a.n; ++j) {
-        const float4 v = *reinterpret_cast<const float4*>(a.o[j] + base + i);
-        acc.x = acc.x + v.x;
-        acc.y = acc.y + v.y;
-        acc.z = acc.z + v.z;
-        acc.w = acc.w + v.w;
-      }
+      // every operand's load issued before the first addition
+      float4 v[NMAX];
+#pragma unroll
+      for (int j = 0; j < NMAX; ++j)
+        if (j < a.n) v[j] = *reinterpret_cast<const float4*>(o[j] + i);
+      float4 acc = v[0];
+#pragma unroll
+      for (int j = 1; j < NMAX; ++j)
+        if (j < a.n) {
+          acc.x = acc.x + v[j].x;
+          acc.y = acc.y + v[j].y;
+          acc.z = acc.z + v[j].z;
+          acc.w = acc.w + v[j].w;
+        }
       acc.x = acc.x / a.div;
       acc.y = acc.y / a.div;
       acc.z = acc.z / a.div;
       acc.w = acc.w / a.div;
-      *reinterpret_cast<float4*>(a.y + base + i) = acc;
+      *reinterpret_cast<float4*>(y + i) = acc;
       vmax = fmaxf(vmax, fmaxf(fmaxf(fabsf(acc.x), fabsf(acc.y)), fmaxf(fabsf(acc.z), fabsf(acc.w))));
     } else {
       // a group of 4 can straddle two channel rows: each sample tests its own column
@@ -519,20 +535,39 @@ __global__ void __launch_bounds__(256) mrf_combine_kernel(MrfCombineArgs a) {
       // samples of a ragged item)
       for (int e = 0; e < 4 && i + e < n; ++e) {
         if ((t + e) % a.L >= len_b) continue;
-        float acc = a.o[0][base + i + e];
-        for (int j = 1; j < a.n; ++j) acc = acc + a.o[j][base + i + e];
-        a.y[base + i + e] = acc / a.div;
+        float acc = o[0][i + e];
+        for (int j = 1; j < NMAX; ++j)
+          if (j < a.n) acc = acc + o[j][i + e];
+        y[i + e] = acc / a.div;
         vmax = fmaxf(vmax, fabsf(acc / a.div));
       }
     }
   }
-  if (a.amax_out) amax_commit(vmax, a.amax_out, b);
+}
+
+__global__ void __launch_bounds__(256) mrf_combine_kernel(MrfCombineArgs a) {
+  const int b = blockIdx.y;
+  float vmax = 0.f;  // max |stored value| (f16x3 consumers: a.amax_out)
+  if (a.n <= 3)
+    mrf_combine_body<3>(a, b, vmax);
+  else
+    mrf_combine_body<kMrfCombineMax>(a, b, vmax);
+  if (!a.amax_out) return;
+  __shared__ float wmax[4];
+  vmax = wave_max(vmax);
+  if ((threadIdx.x & 63) == 0) wmax[threadIdx.x >> 6] = vmax;
+  __syncthreads();
+  if (threadIdx.x < 64) amax_commit(threadIdx.x < 4 ? wmax[threadIdx.x] : 0.f, a.amax_out, b);
 }
 
 hipError_t launch_mrf_combine(const MrfCombineArgs& a, int batch, hipStream_t stream) {
-  if (a.n < 1 || a.n > kMrfCombineMax) return hipErrorInvalidValue;
+  if (a.n < 1 || a.n > kMrfCombineMax || batch < 1) return hipErrorInvalidValue;
+  if ((int64_t)a.C * a.L >= (int64_t{1} << 30)) return hipErrorInvalidValue;
   const int64_t n4 = ((int64_t)a.C * a.L + 3) / 4;
-  const int gx = (int)std::min<int64_t>((n4 + 255) / 256, 4096);
+  // about two blocks per CU over the whole batch (the launch is HBM-bound: 256 CUs x 2 x 256
+  // threads keep enough float4 loads in flight), at least one block per item
+  const int64_t cap = std::max<int64_t>(1, HFG_COMBINE_BLOCKS / batch);
+  const int gx = (int)std::min<int64_t>((n4 + 255) / 256, cap);
   mrf_combine_kernel<<<dim3(gx, batch), dim3(256), 0, stream>>>(a);
   return hipGetLastError();
 }
