@@ -126,10 +126,10 @@ __device__ __forceinline__ float exp2i(int e) { return __builtin_bit_cast(float,
 // kAmaxSpread words (amax_commit), all uniform loads
 __device__ __forceinline__ int x3_exp_slot(const uint32_t* slots, int b) {
   if (!slots) return 0;
-  const uint32_t* s = slots + (size_t)b * kAmaxSpread;
+  const uint32_t* s = slots + (size_t)b * kAmaxSlotWords;
   uint32_t m = 0;
 #pragma unroll
-  for (int i = 0; i < kAmaxSpread; ++i) m = max(m, s[i]);
+  for (int i = 0; i < kAmaxSpread; ++i) m = max(m, s[i * kAmaxLineWords]);
   return x3_exp(__builtin_bit_cast(float, m));
 }
 

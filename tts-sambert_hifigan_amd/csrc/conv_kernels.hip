@@ -488,9 +488,9 @@ hipError_t launch_stage_lengths(const int32_t* lens, int B, const StageLenParams
 // sequential schedule's epilogue running sum, so the result is bitwise the same.
 // float4 over [B][C][L] rows (L % 4 == 0) with a scalar tail; columns past len[b] skipped.
 // An item holds < 2^30 elements (the C ABI's limit), so offsets within it are 32-bit.  The
-// grid is capped near two blocks per CU and each block folds its max into one atomic: the
-// item's kAmaxSpread scale words sit in one L2 channel, and one atomic per wave of a grid
-// that finishes all at once serialised there (round 6: 48 us for 8192 waves at C1).
+// grid is capped near two blocks per CU and each block folds its max into one atomic: a grid
+// that finishes all at once queues its scale atomics on the item's slot lines (kernels.h;
+// round 6: 48 us for 8192 waves on the 2-line slots at C1).
 #ifndef HFG_COMBINE_BLOCKS
 #define HFG_COMBINE_BLOCKS 512
 #endif

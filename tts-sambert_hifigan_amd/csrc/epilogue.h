@@ -55,14 +55,14 @@ __device__ __forceinline__ float wave_max(float m) {
 }
 // fold a lane's max |value| into item b's producer slot: one vector atomic per wave (the
 // slots are zeroed by the host before the forward; non-negative floats order like their bit
-// patterns).  An item's slot is kAmaxSpread words and each wave updates the one its block
-// and wave index select, so same-address atomics do not serialise a whole grid; the
-// consumer takes the max of the kAmaxSpread words (x3_exp_slot).
+// patterns).  An item's slot is kAmaxSpread words on separate 128-B lines and each wave
+// updates the one its block and wave index select, so same-line atomics do not serialise a
+// whole grid (kernels.h); the consumer takes the max of the kAmaxSpread words (x3_exp_slot).
 __device__ __forceinline__ void amax_commit(float m, uint32_t* slots, int b) {
   m = wave_max(m);
   const unsigned blk = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
   const unsigned w = blk * (blockDim.x >> 6) + (threadIdx.x >> 6);
-  uint32_t* slot = slots + (size_t)b * kAmaxSpread + (w & (kAmaxSpread - 1));
+  uint32_t* slot = slots + (size_t)b * kAmaxSlotWords + (w & (kAmaxSpread - 1)) * kAmaxLineWords;
   if ((threadIdx.x & 63) == 0) atomicMax(slot, __builtin_bit_cast(uint32_t, m));
 }
 

@@ -1007,7 +1007,7 @@ int n_bufs(const hfg_handle* h, int64_t B, int64_t T, bool conc_ok) {
 int n_slots(const hfg_handle* h) { return (int)h->layers.size() + 2 * h->cfg.n_up + 4; }
 size_t slots_bytes(const hfg_handle* h, int64_t B) {
   if (h->fmt != hfg::kFmtF16) return 0;
-  return ((size_t)n_slots(h) * (size_t)B * hfg::kAmaxSpread * sizeof(uint32_t) + 255) & ~(size_t)255;
+  return ((size_t)n_slots(h) * (size_t)B * hfg::kAmaxSlotWords * sizeof(uint32_t) + 255) & ~(size_t)255;
 }
 // workspace of one forward_impl call (one batch half)
 size_t ws_part_bytes(const hfg_handle* h, int64_t B, int64_t T, bool conc_ok = false) {
@@ -1060,7 +1060,7 @@ struct Slots {
       overflow = true;
       return nullptr;
     }
-    return base + (size_t)(next++) * (size_t)B * hfg::kAmaxSpread;
+    return base + (size_t)(next++) * (size_t)B * hfg::kAmaxSlotWords;
   }
   bool overflow = false;
 };

@@ -22,9 +22,14 @@ constexpr float kLReluSlope = 0.1f;  // F.leaky_relu(x, 0.1), models/hifigan.py:
 constexpr int kFmtBf16 = 0;
 constexpr int kFmtF16 = 1;
 constexpr int kX3ExpMax = 60;
-// words per (producer launch, batch item) scale slot: waves fold their max into one of them
-// (spread to avoid same-address atomic serialisation); consumers take the max of all
-constexpr int kAmaxSpread = 64;
+// (producer launch, batch item) scale slot: waves fold their max into one of kAmaxSpread
+// words, each on its own 128-B line (kAmaxLineWords apart); consumers take the max of all.
+// Device-scope atomics on one line serialise at ~4.7 ns each on MI355X whatever the word
+// (tests/tools/atomic_probe.hip: 8192 waves into one line 40 us, into 64 lines 3 us), so the
+// round-5 layout (64 words on 2 lines) put a whole single-round grid's commits in a queue.
+constexpr int kAmaxSpread = 16;
+constexpr int kAmaxLineWords = 32;
+constexpr int kAmaxSlotWords = kAmaxSpread * kAmaxLineWords;
 
 // One implicit-GEMM convolution launch:
 //   out[b][m][n] = bias[m] + sum_{ci, j} Wt[m][ci][j] * act_in(x[b][ci][n + off + j*dil])
