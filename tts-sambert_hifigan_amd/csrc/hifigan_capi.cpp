@@ -1468,10 +1468,17 @@ int run_mrf(hfg_handle* h, Launcher& ln, const Stage& st, const float* X, int64_
     for (int j = 1; j < c.n_res && e == hipSuccess; ++j)
       e = hipStreamWaitEvent(h->rb_aux[ln.part][j - 1], h->rb_fork[ln.part], 0);
     if (e != hipSuccess) return hip_fail(e, "ResBlock fork");
+    // the ResBlock with the most work (largest kernel-size sum over its dilations) stays on
+    // the caller's stream: the aux streams start only after the fork event's cross-queue
+    // signal (~10-20 us after the producing launch ends) and the join waits on theirs, so
+    // the chain that finishes last should be the one that pays neither (round 6, C1 traces)
+    int j_main = 0;
+    for (int j = 1; j < c.n_res; ++j)
+      if (c.res_kernels[j] * c.n_dil[j] > c.res_kernels[j_main] * c.n_dil[j_main]) j_main = j;
     int idx = 0;
-    for (int j = 0; j < c.n_res; ++j) {
-      Launcher lj{h, j == 0 ? ln.stream : h->rb_aux[ln.part][j - 1], ln.part, ln.seq, c.n_res,
-                  ln.sl};
+    for (int j = 0, aux = 0; j < c.n_res; ++j) {
+      Launcher lj{h, j == j_main ? ln.stream : h->rb_aux[ln.part][aux++], ln.part, ln.seq,
+                  c.n_res, ln.sl};
       rc = run_one_rb(h, lj, st, j, idx, X, B, L, conc->R[j], conc->Tb[j], conc->O[j], 0, lens,
                       ax, nullptr);
       if (rc) return rc;
