@@ -347,6 +347,14 @@ conv_post4_tanh(const float* __restrict__ x, int64_t x_bs, int C, int L, const f
         q[e][s] = *reinterpret_cast<const f4*>(xb + off);
       }
     }
+    // every load of the batch issued before the first use: left alone, the compiler sank
+    // each channel's loads past the loop-exit test below to their uses (28 VGPRs, one memory
+    // round trip per channel); an empty asm that takes every value pins them here (same-box
+    // C1 / streaming-chunk A/B: -0.5 to -2 %, profiles/r06/c1/c1_ab_post.txt)
+#pragma unroll
+    for (int e = 0; e < CB; ++e)
+#pragma unroll
+      for (int s = 0; s < 3; ++s) asm volatile("" : "+v"(q[e][s]));
 #pragma unroll
     for (int e = 0; e < CB; ++e) {
       if (c0 + e >= C) break;
