@@ -276,3 +276,37 @@ def test_tall_areg_tile_bitwise(pkg, dev, precision):
     assert not any(", 4, 1, 2, 4, 2," in k for k in names["0"])
     for a, b in zip(outs["0"], outs["1"]):
         assert torch.equal(a, b), (a - b).abs().max()
+
+
+@pytest.mark.parametrize("precision", ["f16x3", "fp32"])
+def test_four_resblocks_concurrent_combine(pkg, dev, precision):
+    """An MRF of four ResBlocks (the reference constructor takes any list,
+    models/hifigan.py:178-190) through the concurrent schedule: mrf_combine's general
+    operand path (more than three outputs) and a caller's-stream ResBlock that is not the
+    last one (the one with the largest kernel size x dilation count, here k = 7 x 3).
+    Bitwise the sequential schedule, ragged items bitwise their solo runs, and the oracle
+    within 1e-4."""
+    from oracle import config as C, hifigan_torch as H
+    cfg = C.GenConfig(upsample_rates=[4, 4], upsample_kernel_sizes=[8, 8],
+                      upsample_initial_channel=128, resblock_kernel_sizes=[3, 5, 7, 11],
+                      resblock_dilation_sizes=[[1, 3], [1, 2], [1, 3, 5], [1]])
+    sd = C.make_state_dict(cfg, seed=41)
+    lens = [50, 37]
+    mel = torch.randn(2, 80, 50, generator=torch.Generator().manual_seed(41))
+    outs = {}
+    for mode in ("0", "1"):
+        gen = _gen(pkg, cfg, sd, dev, precision, {"RB_CONC": mode})
+        with torch.no_grad():
+            outs[mode] = gen(mel.to(dev), lengths=lens)
+            if mode == "1":
+                for b, n in enumerate(lens):
+                    solo = gen(mel[b:b + 1, :, :n].contiguous().to(dev))
+                    assert torch.equal(outs[mode][b:b + 1, :, :solo.shape[-1]], solo), b
+        torch.cuda.synchronize()
+    assert torch.equal(outs["0"], outs["1"])
+    err = 0.0
+    for b, n in enumerate(lens):
+        ref = H.generator_forward(H.to_torch_state(sd), cfg, mel[b:b + 1, :, :n])
+        err = max(err, (outs["1"][b:b + 1, :, :ref.shape[-1]].cpu() - ref).abs().max().item())
+    print(f"\nfour ResBlocks [{precision}] concurrent vs oracle {err:.2e}")
+    assert err < ATOL
