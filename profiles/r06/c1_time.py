@@ -1,6 +1,7 @@
 """C1 latency (V1, mel [1, 80, 256]) of the drop-in module: eager and hipGraph replay, median
 of 5 rounds of 20 forwards, plus the wav checksum (same-box library A/Bs, round 6).
-usage: python profiles/r06/c1_time.py [precision] [frames] [batch]"""
+usage: python profiles/r06/c1_time.py [precision] [frames] [batch] [KNOB=VALUE ...]
+(schedule overrides, hfg_debug_schedule_set, applied before the handle is created)"""
 import os
 import sys
 import time
@@ -19,9 +20,14 @@ B = int(sys.argv[3]) if len(sys.argv) > 3 else 1
 dev = torch.device("cuda:0")
 cfg = S.PRESETS["v1"]
 sd = {k: torch.from_numpy(v) for k, v in S.random_state_dict(cfg, seed=0).items()}
+knobs = [a.split("=") for a in sys.argv[4:]]
+for k, v in knobs:
+    pkg.schedule_override(k, int(v))
 gen = pkg.HiFiGANGenerator(**cfg.kwargs(), precision=prec).eval()
 gen.load_state_dict(sd)
 gen = gen.to(dev)
+gen.hip_handle(dev)
+pkg.schedule_clear()
 mel = torch.randn(B, 80, T, generator=torch.Generator().manual_seed(1234)).to(dev)
 
 
@@ -52,5 +58,5 @@ with torch.no_grad():
     ref = gen(mel)
     torch.cuda.synchronize(dev)
     ck = int(pkg._lib.checksum32([ref])[0]) & 0xffffffff
-print(f"{prec} B={B} T={T} eager {eager * 1e3:.3f} ms graph {graph * 1e3:.3f} ms "
+print(f"{prec} B={B} T={T} {' '.join(sys.argv[4:])} eager {eager * 1e3:.3f} ms graph {graph * 1e3:.3f} ms "
       f"graph==eager {bool(torch.equal(wav, ref))} sum {ck:08x}")
