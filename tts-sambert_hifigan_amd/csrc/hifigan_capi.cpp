@@ -981,13 +981,19 @@ Shapes shapes_for(const hfg_handle* h, int64_t B, int64_t T) {
 size_t lens_table_bytes(const hfg_handle* h, int64_t B) {
   return (((size_t)(h->cfg.n_up + 1) * (size_t)B * sizeof(int32_t)) + 255) & ~(size_t)255;
 }
-// concurrent ResBlocks for a stage whose layer grids leave CUs idle: fewer tile-3 blocks
-// (128 rows x 256 columns) per conv than the chip's 512 slots
+// concurrent ResBlocks for a stage whose grids leave CUs idle: fewer tile-3 blocks (128 rows
+// x 256 columns) per conv than HFG_CONC_BLOCKS.  512 (the chip's tile-3 slots) until round 6;
+// with the cheaper mrf_combine, 2048 also takes the whole-ResBlock stages of mid-size single-
+// stream forwards (same-box sweep, profiles/r06/c1/c1_ab_cb.txt: 4 x 512 frames -3.7 %,
+// 32 x 62 -1.6 %, 1 x 4096 -0.8 %, 1 x 8192 and 16 x 256 unchanged; 4096 cost 1 x 8192 +1.2 %)
+#ifndef HFG_CONC_BLOCKS
+#define HFG_CONC_BLOCKS 2048
+#endif
 bool stage_conc(const hfg_handle* h, const Stage& st, int64_t B, int64_t L) {
   const int n_res = h->cfg.n_res;
   if (h->rb_conc == 0 || st.thin || n_res < 2 || n_res > hfg::kMrfCombineMax) return false;
   if (h->rb_conc == 1) return true;
-  return B * ((L + 255) / 256) * ((st.C + 127) / 128) < 512;
+  return B * ((L + 255) / 256) * ((st.C + 127) / 128) < HFG_CONC_BLOCKS;
 }
 bool any_conc(const hfg_handle* h, int64_t B, int64_t T) {
   if (h->mrf_only) return false;
